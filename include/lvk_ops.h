@@ -1,0 +1,66 @@
+/* include/lvk_ops.h -- operator-level C ABI of llama.vk_amd (secondary boundary).
+ *
+ * The reference exposes its quantization codecs through quantize_fns_t /
+ * ggml_internal_get_quantize_fn (reference ggml.h:803-814, ggml.c:6489-6508)
+ * and its ops through the ggml graph API (ggml.h:500-611).  These entry points
+ * run the corresponding MI355X kernels on host buffers (H2D, kernel, D2H) so
+ * each op can be pinned against the CPU oracle in isolation.  `type` is the
+ * ggjt ftype id: 2 = Q4_0, 3 = Q4_1.  All functions return 0 on success and a
+ * negative value on failure (message on stderr).
+ */
+#ifndef LVK_OPS_H
+#define LVK_OPS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#define LVK_API __attribute__((visibility("default")))
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* number of visible GPUs (0 when none); never fails */
+LVK_API int lvk_device_count(void);
+/* version string of the library */
+LVK_API const char * lvk_version(void);
+
+/* quantize_row_q (ggml.c:621-685 / 847-920): x[n][k] -> n rows of blocks in
+ * the reference block layout (20 / 24 bytes per 32 values) */
+LVK_API int lvk_quantize_rows(int type, const float * x, int n, int k, void * y);
+
+/* y[t][r] = vec_dot_q(k, w_row r, quantize_row_q(x[t]))  for r < m, t < n
+ * (ggml_compute_forward_mul_mat_q_f32, ggml.c:6510-6696).  w: m rows in the
+ * file block layout. */
+LVK_API int lvk_mul_mat_q(int type, const void * w, int m, int k, const float * x, int n, float * y);
+
+/* same with the fused RMSNorm prologue: y[t][r] = dot(w_r, quant(g * rms_norm(x[t]))) */
+LVK_API int lvk_mul_mat_q_norm(int type, const void * w, int m, int k, const float * g, const float * x, int n,
+                               float * y);
+
+/* one layer's attention block on an f16 KV cache (llama.cpp:1010-1061):
+ * kc [n_ctx][n_embd] f16, vc [n_embd][n_ctx] f16, q [n][n_embd] f32 (post-RoPE)
+ * -> out [n][n_embd] f32 (merged heads, before the Wo quantization) */
+LVK_API int lvk_attention(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
+                          int n_ctx, int n_past, int n, float * out);
+
+/* y[t] = g * rms_norm(x[t]) (ggml.c:6024-6080 + llama.cpp:984) */
+LVK_API int lvk_rms_norm_mul(const float * x, const float * g, int k, int n, float * y);
+
+/* decode-step profiling of a llama_context: when enabled, every eval records
+ * HIP events around each kernel class (0 embed, 1 qkv, 2 attention, 3 wo,
+ * 4 w1|w3, 5 w2, 6 lm_head) and accumulates device ms, launches and
+ * algorithmic weight bytes. */
+struct llama_context;
+LVK_API void lvk_set_profiling(struct llama_context * ctx, int on);
+LVK_API int lvk_get_profile(struct llama_context * ctx, double * ms, long * launches, double * bytes, int n);
+LVK_API void lvk_reset_profile(struct llama_context * ctx);
+/* bytes of quantized weights resident in HBM for this context's model */
+LVK_API size_t lvk_weight_bytes(struct llama_context * ctx);
+/* 1 = replay the captured decode graph for single-token evals (default), 0 = eager */
+LVK_API void lvk_set_graph(struct llama_context * ctx, int on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,66 @@
+// lvk_device.h -- gfx950 device helpers shared by the llama.vk_amd kernels.
+//
+// Numerics contract: every kernel is compiled with
+// -ffp-contract=off; fmaf appears exactly where the reference AVX2 code uses
+// _mm256_fmadd_ps; float div/sqrt are the correctly rounded sequences hipcc
+// emits by default on gfx950; f32->f16 is IEEE RNE (v_cvt_f16_f32), matching
+// F16C _cvtss_sh(x, 0) (ggml.c:182-183).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lvk {
+
+constexpr int QK = 32;    // elements per quant block (ggml.c:416)
+constexpr int WAVE = 64;  // CDNA wavefront
+
+__device__ __forceinline__ uint16_t f32_to_f16(float x) {
+    _Float16 h = (_Float16) x;   // v_cvt_f16_f32, round-to-nearest-even
+    return __builtin_bit_cast(uint16_t, h);
+}
+__device__ __forceinline__ float f16_to_f32(uint16_t h) {
+    return (float) __builtin_bit_cast(_Float16, h);   // exact
+}
+
+// quad_perm DPP broadcast of lane k (0..3) of each 4-lane quad
+template <int K>
+__device__ __forceinline__ float quad_bcast(float v) {
+    constexpr int ctrl = K | (K << 2) | (K << 4) | (K << 6);
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quad_get(float v, int k) {
+    switch (k) {
+        case 0: return quad_bcast<0>(v);
+        case 1: return quad_bcast<1>(v);
+        case 2: return quad_bcast<2>(v);
+        default: return quad_bcast<3>(v);
+    }
+}
+
+// signed int4 x int4 8-way dot (v_dot8_i32_i4)
+__device__ __forceinline__ int dot8(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_sdot8((int) a, (int) b, 0, false);
+}
+// unsigned u4 x u4 8-way dot (v_dot8_u32_u4)
+__device__ __forceinline__ int udot8(uint32_t a, uint32_t b) {
+    return (int) __builtin_amdgcn_udot8(a, b, 0u, false);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// streamed-once weight loads: non-temporal (nt) global_load_dwordx4
+__device__ __forceinline__ uint4 ld_nt(const uint4 * p) {
+    const u32x4 v = __builtin_nontemporal_load((const u32x4 *) p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ double warp_sum_d(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+    for (int o = 32; o > 0; o >>= 1) { const float w = __shfl_xor(v, o); v = w > v ? w : v; }
+    return v;
+}
+
+}  // namespace lvk

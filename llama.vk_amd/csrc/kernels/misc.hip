@@ -1,0 +1,159 @@
+// misc.hip -- token embedding rows, one-time weight repack into the
+// quad-sliced HBM image, and a standalone activation quantizer.
+#include "lvk_device.h"
+#include "lvk_kernels.h"
+
+namespace lvk {
+
+namespace {
+
+// get_rows + dequantize_row_q4_0/q4_1 AVX2 (ggml.c:6868-6895, 968-1000, 1086-1115)
+__global__ void k_embed(const uint8_t * __restrict__ emb, int type, int E, const int * __restrict__ tokens,
+                        float * __restrict__ x) {
+    const int t = blockIdx.y;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const size_t tok = (size_t) tokens[t];
+    float v;
+    if (type == Q4_0) {
+        const uint8_t * b = emb + tok * (size_t) (E / 32) * 20 + (size_t) (e / 32) * 20;
+        const float d = *(const float *) b;
+        const uint8_t byte = b[4 + (e % 32) / 2];
+        const int qv = (e & 1) ? (byte >> 4) : (byte & 15);
+        v = (float) (qv - 8) * d;
+    } else if (type == Q4_1) {
+        const uint8_t * b = emb + tok * (size_t) (E / 32) * 24 + (size_t) (e / 32) * 24;
+        const float d = *(const float *) b, m = *(const float *) (b + 4);
+        const uint8_t byte = b[8 + (e % 32) / 2];
+        const int qv = (e & 1) ? (byte >> 4) : (byte & 15);
+        const float a = (float) qv * d;
+        v = a + m;
+    } else if (type == 1) {   // f16
+        v = f16_to_f32(((const uint16_t *) emb)[tok * E + e]);
+    } else {                  // f32
+        v = ((const float *) emb)[tok * E + e];
+    }
+    x[(size_t) t * E + e] = v;
+}
+
+// Q4_0 file rows -> quad-sliced image.  One thread per (row, chunk of 8 blocks).
+//   G(i,j) = (qs_i[2j] | qs_i[2j+1] << 8) ^ 0x8888   (elements 4j..4j+3, signed)
+//   X(i,q) = G(i,2q)   | G(i+1,2q)   << 16
+//   Y(i,q) = G(i,2q+1) | G(i+1,2q+1) << 16
+//   nib[g][c][h][4r+q] = {X(8c+4h,q), Y(8c+4h,q), X(8c+4h+2,q), Y(8c+4h+2,q)}
+//   scl[g][c][4r+q]    = {d(8c+q), d(8c+4+q)}
+__global__ void k_repack_q40(const uint8_t * __restrict__ src, int M, int K, uint4 * __restrict__ nib,
+                             float2 * __restrict__ scl) {
+    const int nb = K / 32, C = K / 256;
+    const long idx = (long) blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long) M * C) return;
+    const int row = (int) (idx / C), c = (int) (idx % C);
+    const int g = row / 16, r = row % 16;
+    const uint8_t * rb = src + (size_t) row * nb * 20;
+    float d[8];
+    uint32_t G[8][8];   // [block k][group j]
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint8_t * b = rb + (size_t) (c * 8 + k) * 20;
+        d[k] = *(const float *) b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) G[k][j] = ((uint32_t) b[4 + 2 * j] | ((uint32_t) b[5 + 2 * j] << 8)) ^ 0x8888u;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int lane = 4 * r + q;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i0 = 4 * h, i1 = 4 * h + 2;
+            uint4 v;
+            v.x = G[i0][2 * q] | (G[i0 + 1][2 * q] << 16);
+            v.y = G[i0][2 * q + 1] | (G[i0 + 1][2 * q + 1] << 16);
+            v.z = G[i1][2 * q] | (G[i1 + 1][2 * q] << 16);
+            v.w = G[i1][2 * q + 1] | (G[i1 + 1][2 * q + 1] << 16);
+            nib[(((size_t) g * C + c) * 2 + h) * 64 + lane] = v;
+        }
+        scl[((size_t) g * C + c) * 64 + lane] = make_float2(d[q], d[4 + q]);
+    }
+}
+
+// standalone activation quantizer (quantize_row_q4_0 AVX2, ggml.c:621-685)
+// one thread per block; output split d / qs in the reference nibble layout
+__global__ void k_quantize_q40(const float * __restrict__ x, int N, int K, ActQ out) {
+    const int nb = K / 32;
+    const long idx = (long) blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long) N * nb) return;
+    const int t = (int) (idx / nb), b = (int) (idx % nb);
+    const float * xb = x + (size_t) t * K + (size_t) b * 32;
+    float v[32];
+    float amax = 0.0f;
+#pragma unroll
+    for (int l = 0; l < 32; ++l) { v[l] = xb[l]; const float a = fabsf(v[l]); amax = a > amax ? a : amax; }
+    const float d = amax / 7.0f;
+    const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int l = 0; l < 32; ++l) {
+        const uint32_t q = (uint32_t) ((int) __builtin_rintf(v[l] * id) + 8) & 15u;
+        w[l / 8] |= q << (4 * (l % 8));
+    }
+    out.d[(size_t) t * out.nb + b] = d;
+    out.qs[(size_t) t * out.nb + b] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+}  // namespace
+
+hipError_t launch_embed(const void * emb, int emb_type, int n_embd, const int * tokens, int n, float * x,
+                        hipStream_t s) {
+    dim3 grid((n_embd + 255) / 256, n);
+    hipLaunchKernelGGL(k_embed, grid, dim3(256), 0, s, (const uint8_t *) emb, emb_type, n_embd, tokens, x);
+    return hipGetLastError();
+}
+
+hipError_t launch_repack(const void * src_rows, int qtype, int M, int K, uint4 * nib, void * scl, hipStream_t s) {
+    if (M % 16 || K % 256) return hipErrorInvalidValue;
+    const long n = (long) M * (K / 256);
+    if (qtype == Q4_0) {
+        hipLaunchKernelGGL(k_repack_q40, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s,
+                           (const uint8_t *) src_rows, M, K, nib, (float2 *) scl);
+        return hipGetLastError();
+    }
+    return hipErrorNotSupported;
+}
+
+hipError_t launch_quantize_act(const float * x, int N, int K, int qtype, ActQ out, hipStream_t s) {
+    if (K % 32) return hipErrorInvalidValue;
+    const long n = (long) N * (K / 32);
+    if (qtype == Q4_0) {
+        hipLaunchKernelGGL(k_quantize_q40, dim3((unsigned) ((n + 127) / 128)), dim3(128), 0, s, x, N, K, out);
+        return hipGetLastError();
+    }
+    return hipErrorNotSupported;
+}
+
+}  // namespace lvk
+
+namespace lvk {
+namespace {
+// ggml_compute_forward_rms_norm_f32 (ggml.c:6058-6076) + mul by g, one WG per row
+__global__ __launch_bounds__(256) void k_rmsnorm_rows(const float * __restrict__ x, const float * __restrict__ g,
+                                                      int K, float * __restrict__ y) {
+    __shared__ double red[4];
+    const int t = blockIdx.x;
+    const float * xr = x + (size_t) t * K;
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < K; i += 256) { const float sq = xr[i] * xr[i]; acc += (double) sq; }
+    acc = warp_sum_d(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    const double s = (red[0] + red[1]) + (red[2] + red[3]);
+    const float mean = (float) (s / (double) K);
+    const float scale = 1.0f / sqrtf(mean + 1e-6f);
+    for (int i = threadIdx.x; i < K; i += 256) { const float yn = xr[i] * scale; y[(size_t) t * K + i] = g[i] * yn; }
+}
+}  // namespace
+
+hipError_t launch_rmsnorm_rows(const float * x, const float * g, int K, int n, float * y, hipStream_t s) {
+    hipLaunchKernelGGL(k_rmsnorm_rows, dim3(n), dim3(256), 0, s, x, g, K, y);
+    return hipGetLastError();
+}
+}  // namespace lvk

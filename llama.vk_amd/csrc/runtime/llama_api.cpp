@@ -1,0 +1,323 @@
+// llama_api.cpp -- the drop-in C API (include/llama.h) over the HIP runtime.
+//
+// Semantics follow the reference implementation (llama.cpp:1579-1852):
+// NULL / non-zero returns on failure with the error printed to stderr, the
+// context owns model, KV cache and buffers, logits/embeddings pointers stay
+// valid until the next eval, no thread safety.  Tokenizer and sampler are host
+// code with the reference's exact tie-breaking (same std::priority_queue /
+// std::partial_sort / std::discrete_distribution over std::mt19937).
+#include <cinttypes>
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <queue>
+#include <sys/mman.h>
+
+#include "../../../include/llama.h"
+#include "lvk_context.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// tokenizer: greedy highest-score bigram merging over UTF-8 characters with
+// byte fallback (llama.cpp:1199-1350)
+// ---------------------------------------------------------------------------
+struct Sym {
+    int prev, next;
+    const char * text;
+    size_t n;
+};
+struct Bigram {
+    int left, right;
+    float score;
+    size_t size;
+};
+struct BigramLess {   // max-heap on score, ties: smaller left index first
+    bool operator()(const Bigram & a, const Bigram & b) const {
+        return a.score < b.score || (a.score == b.score && a.left > b.left);
+    }
+};
+
+size_t utf8_char_len(char c) {
+    static const size_t len[16] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 3, 4};
+    return len[(uint8_t) c >> 4];
+}
+
+std::vector<int> tokenize(const lvk::Vocab & vocab, const std::string & text, bool bos) {
+    std::vector<int> out;
+    if (text.empty()) return out;
+    if (bos) out.push_back(1);
+    std::vector<Sym> syms;
+    for (size_t off = 0; off < text.size();) {
+        const size_t n = std::min(text.size() - off, utf8_char_len(text[off]));
+        const int idx = (int) syms.size();
+        syms.push_back({idx - 1, off + n == text.size() ? -1 : idx + 1, text.data() + off, n});
+        off += n;
+    }
+    std::priority_queue<Bigram, std::vector<Bigram>, BigramLess> pq;
+    auto try_add = [&](int l, int r) {
+        if (l == -1 || r == -1) return;
+        const std::string s(syms[l].text, syms[l].n + syms[r].n);
+        auto it = vocab.token_to_id.find(s);
+        if (it == vocab.token_to_id.end() || (size_t) it->second >= vocab.id_to_token.size()) return;
+        pq.push({l, r, vocab.id_to_token[it->second].score, s.size()});
+    };
+    for (size_t i = 1; i < syms.size(); ++i) try_add((int) i - 1, (int) i);
+    while (!pq.empty()) {
+        const Bigram b = pq.top();
+        pq.pop();
+        Sym & L = syms[b.left];
+        Sym & R = syms[b.right];
+        if (L.n == 0 || R.n == 0 || L.n + R.n != b.size) continue;   // stale
+        L.n += R.n;
+        R.n = 0;
+        L.next = R.next;
+        if (R.next >= 0) syms[R.next].prev = b.left;
+        try_add(L.prev, b.left);
+        try_add(b.left, L.next);
+    }
+    for (int i = 0; i != -1; i = syms[i].next) {
+        auto it = vocab.token_to_id.find(std::string(syms[i].text, syms[i].n));
+        if (it == vocab.token_to_id.end()) {
+            for (size_t j = 0; j < syms[i].n; ++j) out.push_back((int) (uint8_t) syms[i].text[j] + 3);
+        } else {
+            out.push_back(it->second);
+        }
+    }
+    return out;
+}
+
+// ---------------------------------------------------------------------------
+// sampler (llama.cpp:1352-1459)
+// ---------------------------------------------------------------------------
+int sample_top_p_top_k(lvk::Context & c, const std::vector<int> & last, int top_k, float top_p, float temp,
+                       float repeat_penalty) {
+    const int n_logits = (int) c.model.hp.n_vocab;
+    const float * pl = c.logits.data() + c.logits.size() - n_logits;
+    if (temp <= 0) {
+        float best = pl[0];
+        int id = 0;
+        for (int i = 1; i < n_logits; ++i)
+            if (pl[i] > best) { best = pl[i]; id = i; }
+        return id;
+    }
+    std::vector<std::pair<float, int>> cand;
+    cand.reserve(n_logits);
+    const float scale = 1.0f / temp;
+    for (int i = 0; i < n_logits; ++i) {
+        if (std::find(last.begin(), last.end(), i) != last.end()) {
+            if (pl[i] < 0.0f) cand.emplace_back(pl[i] * scale * repeat_penalty, i);
+            else cand.emplace_back(pl[i] * scale / repeat_penalty, i);
+        } else {
+            cand.emplace_back(pl[i] * scale, i);
+        }
+    }
+    const int k = top_k > 0 ? std::min(top_k, n_logits) : n_logits;
+    std::partial_sort(cand.begin(), cand.begin() + k, cand.end(),
+                      [](const std::pair<float, int> & a, const std::pair<float, int> & b) { return a.first > b.first; });
+    cand.resize(k);
+    std::vector<float> probs;
+    probs.reserve(cand.size());
+    const float maxl = cand[0].first;
+    double sum = 0.0;
+    for (const auto & kv : cand) {
+        const float p = expf(kv.first - maxl);
+        probs.push_back(p);
+        sum += p;
+    }
+    for (auto & p : probs) p /= sum;
+    if (top_p < 1.0) {
+        double cum = 0.0;
+        for (int i = 0; i < (int) probs.size(); ++i) {
+            cum += probs[i];
+            if (cum >= top_p) {
+                probs.resize(i + 1);
+                cand.resize(i + 1);
+                break;
+            }
+        }
+    }
+    std::discrete_distribution<> dist(probs.begin(), probs.end());
+    return cand[dist(c.rng)].second;
+}
+
+void default_progress(float progress, void * ud) {
+    unsigned * cur = (unsigned *) ud;
+    const unsigned pct = (unsigned) (100 * progress);
+    while (pct > *cur) {
+        ++*cur;
+        fprintf(stderr, ".");
+        fflush(stderr);
+        if (pct >= 100) fprintf(stderr, "\n");
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+struct llama_context_params llama_context_default_params(void) {
+    llama_context_params r;
+    r.n_ctx = 512;
+    r.n_parts = -1;
+    r.seed = 0;
+    r.f16_kv = false;
+    r.logits_all = false;
+    r.vocab_only = false;
+    r.use_mmap = true;
+    r.use_mlock = false;
+    r.embedding = false;
+    r.progress_callback = nullptr;
+    r.progress_callback_user_data = nullptr;
+    return r;
+}
+
+bool llama_mmap_supported(void) { return true; }
+bool llama_mlock_supported(void) { return true; }
+
+struct llama_context * llama_init_from_file(const char * path_model, struct llama_context_params params) {
+    llama_context * ctx = new llama_context;
+    lvk::Context & c = ctx->c;
+    c.t_start_us = lvk::now_us();
+    if (params.seed <= 0) params.seed = (int) time(nullptr);
+    c.rng = std::mt19937(params.seed);
+    unsigned cur_pct = 0;
+    if (!params.progress_callback) {
+        params.progress_callback = default_progress;
+        params.progress_callback_user_data = &cur_pct;
+    }
+    try {
+        if (!params.f16_kv && !params.vocab_only)
+            fprintf(stderr, "llama.vk_amd: f32 KV cache not implemented on the GPU path; using f16 KV\n");
+        hipStream_t ls = nullptr;
+        if (!params.vocab_only) LVK_HIP(hipStreamCreateWithFlags(&ls, hipStreamNonBlocking));
+        lvk::load_model(c.model, path_model, params.vocab_only, ls, params.progress_callback,
+                        params.progress_callback_user_data);
+        if (ls) (void) hipStreamDestroy(ls);
+        c.model.hp.n_ctx = (uint32_t) params.n_ctx;
+        if (!params.vocab_only) {
+            c.init(params);
+            fprintf(stderr, "%s: kv self size  = %7.2f MB\n", __func__, c.kv_bytes() / 1024.0 / 1024.0);
+        }
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "error loading model: %s\n", e.msg.c_str());
+        fprintf(stderr, "%s: failed to load model\n", __func__);
+        delete ctx;
+        return nullptr;
+    }
+    c.t_load_us = lvk::now_us() - c.t_start_us;
+    return ctx;
+}
+
+void llama_free(struct llama_context * ctx) { delete ctx; }
+
+int llama_eval(struct llama_context * ctx, const llama_token * tokens, int n_tokens, int n_past, int n_threads) {
+    (void) n_threads;   // host thread count hint; the forward pass runs on the GPU
+    lvk::Context & c = ctx->c;
+    const int64_t t0 = lvk::now_us();
+    try {
+        c.eval(tokens, n_tokens, n_past);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: failed to eval: %s\n", __func__, e.msg.c_str());
+        return 1;
+    }
+    const int64_t dt = lvk::now_us() - t0;
+    if (n_tokens == 1) { c.t_eval_us += dt; c.n_eval++; }          // llama.cpp:1186-1195
+    else if (n_tokens > 1) { c.t_p_eval_us += dt; c.n_p_eval += n_tokens; }
+    if (!c.has_evaluated_once) {
+        c.t_load_us = lvk::now_us() - c.t_start_us;
+        c.has_evaluated_once = true;
+    }
+    return 0;
+}
+
+int llama_tokenize(struct llama_context * ctx, const char * text, llama_token * tokens, int n_max_tokens,
+                   bool add_bos) {
+    const std::vector<int> res = tokenize(ctx->c.model.vocab, text, add_bos);
+    if (n_max_tokens < (int) res.size()) {
+        fprintf(stderr, "%s: too many tokens\n", __func__);
+        return -((int) res.size());
+    }
+    for (size_t i = 0; i < res.size(); ++i) tokens[i] = res[i];
+    return (int) res.size();
+}
+
+int llama_n_vocab(struct llama_context * ctx) { return (int) ctx->c.model.vocab.id_to_token.size(); }
+int llama_n_ctx(struct llama_context * ctx) { return (int) ctx->c.model.hp.n_ctx; }
+int llama_n_embd(struct llama_context * ctx) { return (int) ctx->c.model.hp.n_embd; }
+float * llama_get_logits(struct llama_context * ctx) { return ctx->c.logits.data(); }
+float * llama_get_embeddings(struct llama_context * ctx) { return ctx->c.embedding.data(); }
+
+const char * llama_token_to_str(struct llama_context * ctx, llama_token token) {
+    if (token >= llama_n_vocab(ctx)) return nullptr;
+    return ctx->c.model.vocab.id_to_token[token].text.c_str();
+}
+
+llama_token llama_token_bos(void) { return 1; }
+llama_token llama_token_eos(void) { return 2; }
+
+llama_token llama_sample_top_p_top_k(struct llama_context * ctx, const llama_token * last_n_tokens_data,
+                                     int last_n_tokens_size, int top_k, float top_p, float temp,
+                                     float repeat_penalty) {
+    lvk::Context & c = ctx->c;
+    const int64_t t0 = lvk::now_us();
+    const std::vector<int> last(last_n_tokens_data, last_n_tokens_data + last_n_tokens_size);
+    const int r = sample_top_p_top_k(c, last, top_k, top_p, temp, repeat_penalty);
+    c.t_sample_us += lvk::now_us() - t0;
+    c.n_sample++;
+    return r;
+}
+
+const uint8_t * llama_get_kv_cache(struct llama_context * ctx) {
+    try { ctx->c.kv_get(); } catch (const lvk::Error & e) { fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str()); }
+    return ctx->c.kv_host.data();
+}
+size_t llama_get_kv_cache_size(struct llama_context * ctx) { return ctx->c.kv_bytes(); }
+int llama_get_kv_cache_token_count(struct llama_context * ctx) { return ctx->c.kv_n; }
+void llama_set_kv_cache(struct llama_context * ctx, const uint8_t * kv_cache, size_t n_size, int n_token_count) {
+    if (n_size != ctx->c.kv_bytes()) {   // LLAMA_ASSERT in the reference (llama.cpp:1696)
+        fprintf(stderr, "llama_set_kv_cache: size mismatch\n");
+        abort();
+    }
+    ctx->c.kv_set(kv_cache, n_size);
+    ctx->c.kv_n = n_token_count;
+}
+
+void llama_print_timings(struct llama_context * ctx) {
+    lvk::Context & c = ctx->c;
+    const int64_t t_end = lvk::now_us();
+    const int n_sample = std::max(1, c.n_sample), n_eval = std::max(1, c.n_eval), n_p_eval = std::max(1, c.n_p_eval);
+    fprintf(stderr, "\n");
+    fprintf(stderr, "%s:        load time = %8.2f ms\n", __func__, c.t_load_us / 1000.0);
+    fprintf(stderr, "%s:      sample time = %8.2f ms / %5d runs   (%8.2f ms per run)\n", __func__, 1e-3 * c.t_sample_us,
+            n_sample, 1e-3 * c.t_sample_us / n_sample);
+    fprintf(stderr, "%s: prompt eval time = %8.2f ms / %5d tokens (%8.2f ms per token)\n", __func__,
+            1e-3 * c.t_p_eval_us, n_p_eval, 1e-3 * c.t_p_eval_us / n_p_eval);
+    fprintf(stderr, "%s:        eval time = %8.2f ms / %5d runs   (%8.2f ms per run)\n", __func__, 1e-3 * c.t_eval_us,
+            n_eval, 1e-3 * c.t_eval_us / n_eval);
+    fprintf(stderr, "%s:       total time = %8.2f ms\n", __func__, (t_end - c.t_start_us) / 1000.0);
+}
+
+void llama_reset_timings(struct llama_context * ctx) {
+    lvk::Context & c = ctx->c;
+    c.t_start_us = lvk::now_us();
+    c.t_sample_us = c.n_sample = 0;
+    c.t_eval_us = c.n_eval = 0;
+    c.t_p_eval_us = c.n_p_eval = 0;
+}
+
+const char * llama_print_system_info(void) {
+    static std::string s;
+    int dev = 0, n = 0;
+    hipDeviceProp_t prop{};
+    if (hipGetDeviceCount(&n) == hipSuccess && n > 0 && hipGetDevice(&dev) == hipSuccess)
+        (void) hipGetDeviceProperties(&prop, dev);
+    s = "HIP = 1 | GPU = ";
+    s += n > 0 ? prop.gcnArchName : "none";
+    s += " | CUs = " + std::to_string(n > 0 ? prop.multiProcessorCount : 0);
+    s += " | HBM = " + std::to_string(n > 0 ? (long long) (prop.totalGlobalMem >> 20) : 0) + " MiB";
+    s += " | WAVE64 = 1 | DOT8_I4 = 1 | KV = f16 | ";
+    return s.c_str();
+}
+
+}  // extern "C"

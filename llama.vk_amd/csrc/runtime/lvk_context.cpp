@@ -1,0 +1,235 @@
+// lvk_context.cpp -- llama_eval on one HIP stream.
+//
+// The reference builds a ~1253-node ggml graph per token and runs it on a CPU
+// thread pool (llama.cpp:927-1137, ggml.c:9230-9651).  Here the same forward
+// pass is 6 fused kernels per layer (+ embedding and lm_head) on one stream:
+//   QKV matvec  (rms_norm*g -> Q4 quantize -> Wq|Wk|Wv -> RoPE -> KV append)
+//   attention   (scores; softmax -> P.V -> Q4 quantize of the merged heads)
+//   Wo matvec   (+ residual)
+//   W1|W3 matvec(rms_norm*g -> quantize -> silu(w1x)*w3x -> Q4 quantize)
+//   W2 matvec   (+ residual)
+// Single-token decode is captured once into a hipGraph; the position and the
+// token come from a 16-byte step block copied to HBM before each replay, so
+// the same graph serves every n_past.
+#include "lvk_context.h"
+
+#include <immintrin.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "../../../include/llama.h"
+
+namespace lvk {
+
+int64_t now_us() {
+    return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+namespace {
+// host F16C conversion, identical to the reference's GGML_FP32_TO_FP16 (ggml.c:183)
+__attribute__((target("f16c"))) uint16_t h_f32_to_f16(float f) { return _cvtss_sh(f, 0); }
+__attribute__((target("f16c"))) float h_f16_to_f32(uint16_t h) { return _cvtsh_ss(h); }
+}  // namespace
+
+void host_fp16_tables(std::vector<uint16_t> & te, std::vector<uint16_t> & ts) {
+    te.resize(65536);
+    ts.resize(65536);
+    for (int i = 0; i < 65536; ++i) {
+        const float f = h_f16_to_f32((uint16_t) i);
+        ts[i] = h_f32_to_f16(f / (1.0f + expf(-f)));
+        te[i] = h_f32_to_f16(expf(f));
+    }
+}
+
+Context::~Context() {
+    if (graph_exec) (void) hipGraphExecDestroy(graph_exec);
+    if (graph) (void) hipGraphDestroy(graph);
+    for (auto & e : ev_pool) { (void) hipEventDestroy(e.first); (void) hipEventDestroy(e.second); }
+    if (sp_h) (void) hipHostFree(sp_h);
+    if (tok_h) (void) hipHostFree(tok_h);
+    if (stream) (void) hipStreamDestroy(stream);
+}
+
+void Context::init(const llama_context_params & p) {
+    n_ctx = p.n_ctx;
+    logits_all = p.logits_all;
+    want_embedding = p.embedding;
+    const HParams & hp = model.hp;
+    const size_t E = hp.n_embd, L = hp.n_layer, V = hp.n_vocab, H = hp.n_head, F = hp.n_ff();
+    const size_t hd = E / H, C = (size_t) n_ctx;
+    if (n_ctx < 64 || n_ctx % 32) throw Error("llama.vk_amd: n_ctx must be a multiple of 32 and >= 64");
+    kc = (uint16_t *) model.alloc(L * C * E * 2);
+    vc = (uint16_t *) model.alloc(L * C * E * 2);
+    LVK_HIP(hipMemset(kc, 0, L * C * E * 2));
+    LVK_HIP(hipMemset(vc, 0, L * C * E * 2));
+    x = (float *) model.alloc(C * E * 4);
+    q16 = (uint16_t *) model.alloc(C * E * 2);
+    scores = (float *) model.alloc(C * H * C * 4);
+    aq_attn.nb = (int) (E / 32);
+    aq_attn.d = (float *) model.alloc(C * (E / 32) * 4);
+    aq_attn.m = (float *) model.alloc(C * (E / 32) * 4);
+    aq_attn.qs = (uint4 *) model.alloc(C * (E / 32) * 16);
+    aq_ffn.nb = (int) (F / 32);
+    aq_ffn.d = (float *) model.alloc(C * (F / 32) * 4);
+    aq_ffn.m = (float *) model.alloc(C * (F / 32) * 4);
+    aq_ffn.qs = (uint4 *) model.alloc(C * (F / 32) * 16);
+    logits_d = (float *) model.alloc(C * V * 4);
+    emb_d = (float *) model.alloc(E * 4);
+    sp_d = (StepParams *) model.alloc(sizeof(StepParams));
+    tok_d = (int *) model.alloc(C * 4);
+    LVK_HIP(hipHostMalloc((void **) &sp_h, sizeof(StepParams), hipHostMallocDefault));
+    LVK_HIP(hipHostMalloc((void **) &tok_h, C * 4, hipHostMallocDefault));
+
+    // fp16 exp / silu tables (ggml.c:2915-2927), built with this host's glibc
+    std::vector<uint16_t> te, ts;
+    host_fp16_tables(te, ts);
+    exp_tab = (uint16_t *) model.alloc(65536 * 2);
+    silu_tab = (uint16_t *) model.alloc(65536 * 2);
+    LVK_HIP(hipMemcpy(exp_tab, te.data(), 65536 * 2, hipMemcpyHostToDevice));
+    LVK_HIP(hipMemcpy(silu_tab, ts.data(), 65536 * 2, hipMemcpyHostToDevice));
+    // RoPE cos/sin table (ggml.c:7209-7213): theta = powf(10000, -i0/n_dims), angle = p*theta
+    std::vector<float2> rt(C * (hd / 2));
+    for (size_t pos = 0; pos < C; ++pos)
+        for (size_t i0 = 0; i0 < hd; i0 += 2) {
+            const float theta = powf(10000.0f, ((float) -(int) i0) / (float) hd);
+            const float ang = (float) (int) pos * theta;
+            rt[pos * (hd / 2) + i0 / 2] = make_float2(cosf(ang), sinf(ang));
+        }
+    rope = (float2 *) model.alloc(rt.size() * sizeof(float2));
+    LVK_HIP(hipMemcpy(rope, rt.data(), rt.size() * sizeof(float2), hipMemcpyHostToDevice));
+
+    LVK_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    logits.reserve(logits_all ? C * V : V);
+    if (want_embedding) embedding.resize(E);
+}
+
+void Context::timed_launch(int cls, double bytes, const std::function<hipError_t()> & fn) {
+    if (!profiling) {
+        LVK_HIP(fn());
+        return;
+    }
+    if (ev_used == ev_pool.size()) {
+        hipEvent_t a, b;
+        LVK_HIP(hipEventCreate(&a));
+        LVK_HIP(hipEventCreate(&b));
+        ev_pool.push_back({a, b});
+        ev_class.push_back(0);
+    }
+    auto & e = ev_pool[ev_used];
+    ev_class[ev_used] = cls;
+    ++ev_used;
+    LVK_HIP(hipEventRecord(e.first, stream));
+    LVK_HIP(fn());
+    LVK_HIP(hipEventRecord(e.second, stream));
+    prof.launches[cls] += 1;
+    prof.bytes[cls] += bytes;
+}
+
+void Context::collect_profile() {
+    for (size_t i = 0; i < ev_used; ++i) {
+        float ms = 0.0f;
+        LVK_HIP(hipEventElapsedTime(&ms, ev_pool[i].first, ev_pool[i].second));
+        prof.ms[ev_class[i]] += ms;
+    }
+    ev_used = 0;
+}
+
+static double qbytes(const QMatrix & w) { return (double) w.M * (w.K / 32) * (w.qtype == Q4_0 ? 20 : 24); }
+
+void Context::enqueue_forward(int n, bool last_only) {
+    const HParams & hp = model.hp;
+    const int E = (int) hp.n_embd, H = (int) hp.n_head, hd = E / H, V = (int) hp.n_vocab;
+    (void) V;
+    const size_t CE = (size_t) n_ctx * E;
+    timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_d, n, x, stream); });
+    for (size_t il = 0; il < model.layers.size(); ++il) {
+        const Layer & ly = model.layers[il];
+        MvLaunch a;
+        a.w = ly.wqkv; a.x = x; a.g = ly.attn_norm; a.sp = sp_d; a.n_tokens = n;
+        a.q16 = q16; a.kc = kc + il * CE; a.vc = vc + il * CE; a.rope.cs = rope;
+        a.n_embd = E; a.head_dim = hd; a.n_ctx = n_ctx;
+        timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return launch_matvec(a, PRO_NORM, EPI_QKV, stream); });
+        AttnLaunch at{q16, kc + il * CE, vc + il * CE, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
+        timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
+        MvLaunch b;
+        b.w = ly.wo; b.xq = aq_attn; b.y = x; b.sp = sp_d; b.n_tokens = n;
+        timed_launch(K_WO, qbytes(ly.wo), [&] { return launch_matvec(b, PRO_ACTQ, EPI_RESID, stream); });
+        MvLaunch c;
+        c.w = ly.w13; c.x = x; c.g = ly.ffn_norm; c.sp = sp_d; c.n_tokens = n; c.silu_tab = silu_tab; c.out_q = aq_ffn;
+        timed_launch(K_W13, qbytes(ly.w13), [&] { return launch_matvec(c, PRO_NORM, EPI_SWIGLU, stream); });
+        MvLaunch d;
+        d.w = ly.w2; d.xq = aq_ffn; d.y = x; d.sp = sp_d; d.n_tokens = n;
+        timed_launch(K_W2, qbytes(ly.w2), [&] { return launch_matvec(d, PRO_ACTQ, EPI_RESID, stream); });
+    }
+    MvLaunch o;
+    o.w = model.output; o.x = x; o.g = model.norm; o.sp = sp_d; o.y = logits_d;
+    o.tok0 = last_only ? n - 1 : 0;
+    o.n_tokens = last_only ? 1 : n;
+    timed_launch(K_LMHEAD, qbytes(model.output), [&] { return launch_matvec(o, PRO_NORM, EPI_STORE, stream); });
+    if (want_embedding)
+        LVK_HIP(launch_rmsnorm_rows(x + (size_t) (n - 1) * E, model.norm, E, 1, emb_d, stream));
+}
+
+void Context::build_graph() {
+    LVK_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    try {
+        enqueue_forward(1, true);
+    } catch (...) {
+        hipGraph_t g;
+        (void) hipStreamEndCapture(stream, &g);
+        throw;
+    }
+    LVK_HIP(hipStreamEndCapture(stream, &graph));
+    LVK_HIP(hipGraphInstantiate(&graph_exec, graph, nullptr, nullptr, 0));
+}
+
+void Context::eval(const int * tokens, int n, int n_past) {
+    const HParams & hp = model.hp;
+    const int V = (int) hp.n_vocab;
+    if (n <= 0 || n_past < 0 || n_past + n > n_ctx) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
+    for (int i = 0; i < n; ++i)
+        if (tokens[i] < 0 || tokens[i] >= V) throw Error("llama.vk_amd: token id out of range");
+    sp_h->n_past = n_past;
+    sp_h->n_tokens = n;
+    std::memcpy(tok_h, tokens, sizeof(int) * (size_t) n);
+    LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
+    LVK_HIP(hipMemcpyAsync(tok_d, tok_h, sizeof(int) * (size_t) n, hipMemcpyHostToDevice, stream));
+    const bool last_only = !logits_all;
+    if (n == 1 && last_only && use_graph && !profiling) {
+        if (!graph_exec) build_graph();
+        LVK_HIP(hipGraphLaunch(graph_exec, stream));
+    } else {
+        enqueue_forward(n, last_only);
+    }
+    const int rows = last_only ? 1 : n;
+    logits.resize((size_t) rows * V);
+    LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost, stream));
+    if (want_embedding) {
+        embedding.resize(hp.n_embd);
+        LVK_HIP(hipMemcpyAsync(embedding.data(), emb_d, sizeof(float) * hp.n_embd, hipMemcpyDeviceToHost, stream));
+    }
+    LVK_HIP(hipStreamSynchronize(stream));
+    if (profiling) collect_profile();
+}
+
+size_t Context::kv_bytes() const {
+    return 2u * (size_t) model.hp.n_layer * n_ctx * model.hp.n_embd * 2u;
+}
+
+void Context::kv_get() {
+    const size_t half = kv_bytes() / 2;
+    kv_host.resize(kv_bytes());
+    LVK_HIP(hipMemcpy(kv_host.data(), kc, half, hipMemcpyDeviceToHost));
+    LVK_HIP(hipMemcpy(kv_host.data() + half, vc, half, hipMemcpyDeviceToHost));
+}
+
+void Context::kv_set(const uint8_t * src, size_t n) {
+    if (n != kv_bytes()) throw Error("llama_set_kv_cache: size mismatch");
+    const size_t half = n / 2;
+    LVK_HIP(hipMemcpy(kc, src, half, hipMemcpyHostToDevice));
+    LVK_HIP(hipMemcpy(vc, src + half, half, hipMemcpyHostToDevice));
+}
+
+}  // namespace lvk

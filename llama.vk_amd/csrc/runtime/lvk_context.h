@@ -1,0 +1,93 @@
+// lvk_context.h -- one inference context: device KV cache, scratch, the
+// launch sequence of llama_eval on a HIP stream and the captured decode graph.
+#pragma once
+#include "lvk_model.h"
+
+#include <array>
+#include <chrono>
+#include <functional>
+
+struct llama_context_params;
+
+namespace lvk {
+
+// kernel classes timed by the profiler (events around every launch of a class)
+enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_WO, K_W13, K_W2, K_LMHEAD, K_NCLASS };
+
+struct Profile {
+    std::array<double, K_NCLASS> ms{};       // accumulated device time
+    std::array<long, K_NCLASS> launches{};   // launches accumulated
+    std::array<double, K_NCLASS> bytes{};    // algorithmic HBM bytes accumulated
+};
+
+struct Context {
+    Model model;
+    int n_ctx = 512;
+    bool logits_all = false;
+    bool want_embedding = false;
+    hipStream_t stream = nullptr;
+
+    // device state
+    uint16_t * kc = nullptr;     // [L][n_ctx][E]
+    uint16_t * vc = nullptr;     // [L][E][n_ctx]
+    float * x = nullptr;         // residual stream [n_ctx][E]
+    uint16_t * q16 = nullptr;    // [n_ctx][E]
+    float * scores = nullptr;    // [n_ctx][H][n_ctx]
+    ActQ aq_attn;                // [n_ctx][E/32]
+    ActQ aq_ffn;                 // [n_ctx][F/32]
+    float * logits_d = nullptr;  // [n_ctx][V]
+    float * emb_d = nullptr;     // [E]
+    uint16_t * exp_tab = nullptr;
+    uint16_t * silu_tab = nullptr;
+    float2 * rope = nullptr;     // [n_ctx][hd/2]
+    StepParams * sp_d = nullptr;
+    int * tok_d = nullptr;       // [n_ctx]
+    StepParams * sp_h = nullptr; // pinned
+    int * tok_h = nullptr;       // pinned
+
+    // decode graph (N = 1, last-token logits)
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    bool use_graph = true;
+
+    // host-visible results
+    std::vector<float> logits;
+    std::vector<float> embedding;
+    std::vector<uint8_t> kv_host;
+    int kv_n = 0;
+    std::mt19937 rng;
+
+    // timings (llama.cpp:1186-1195)
+    int64_t t_start_us = 0, t_load_us = 0, t_sample_us = 0, t_eval_us = 0, t_p_eval_us = 0;
+    int n_sample = 0, n_eval = 0, n_p_eval = 0;
+    bool has_evaluated_once = false;
+
+    // profiling
+    bool profiling = false;
+    Profile prof;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+    std::vector<int> ev_class;
+    size_t ev_used = 0;
+
+    ~Context();
+    void init(const llama_context_params & p);
+    void eval(const int * tokens, int n, int n_past);
+    void enqueue_forward(int n, bool last_only);
+    void build_graph();
+    void kv_get();
+    void kv_set(const uint8_t * src, size_t n);
+    size_t kv_bytes() const;
+    void timed_launch(int cls, double bytes, const std::function<hipError_t()> & fn);
+    void collect_profile();
+};
+
+int64_t now_us();
+// fp16 exp / silu tables (ggml.c:2915-2927) built with this host's glibc expf
+void host_fp16_tables(std::vector<uint16_t> & exp_tab, std::vector<uint16_t> & silu_tab);
+
+}  // namespace lvk
+
+// the opaque handle of the C API (include/llama.h)
+struct llama_context {
+    lvk::Context c;
+};

@@ -1,0 +1,77 @@
+// lvk_model.h -- host-side model/context structures of the llama.vk_amd runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../kernels/lvk_kernels.h"
+
+#define LVK_HIP(call)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess) throw lvk::Error(std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+namespace lvk {
+
+struct Error {
+    std::string msg;
+    explicit Error(std::string m) : msg(std::move(m)) {}
+};
+
+// llama_hparams (llama_internal.h / llama.cpp:751-780)
+struct HParams {
+    uint32_t n_vocab = 32000, n_ctx = 512, n_embd = 4096, n_mult = 256, n_head = 32, n_layer = 32,
+             n_rot = 64, ftype = 2;
+    uint32_t n_ff() const { return ((2 * (4 * n_embd) / 3 + n_mult - 1) / n_mult) * n_mult; }  // llama.cpp:771
+};
+
+struct Vocab {
+    struct Tok { std::string text; float score; };
+    std::vector<Tok> id_to_token;
+    std::map<std::string, int> token_to_id;
+};
+
+// one device allocation owned by the model
+struct DevBuf {
+    void * p = nullptr;
+    size_t n = 0;
+};
+
+struct Layer {
+    float * attn_norm = nullptr;   // [E] f32
+    float * ffn_norm = nullptr;    // [E] f32
+    QMatrix wqkv;                  // fused [3E][E]: wq | wk | wv rows
+    QMatrix wo;                    // [E][E]
+    QMatrix w13;                   // fused [2F][E]: per 32-row block b: w1 rows, then w3 rows
+    QMatrix w2;                    // [E][F]
+};
+
+struct Model {
+    HParams hp;
+    Vocab vocab;
+    int qtype = Q4_0;              // weight format of the layer matrices
+    int emb_type = Q4_0;           // tok_embeddings storage type (ggjt ftype id)
+    void * tok_emb = nullptr;      // device, file layout
+    float * norm = nullptr;        // [E]
+    QMatrix output;                // [V][E]
+    std::vector<Layer> layers;
+    std::vector<DevBuf> bufs;      // owned device memory
+    size_t weight_bytes = 0;       // bytes of weights resident in HBM (quad-sliced images)
+    size_t file_bytes = 0;
+    double load_ms = 0;
+
+    void * alloc(size_t n);
+    ~Model();
+};
+
+// Load a ggjt v1 (or ggmf/ggml vocab-only) file.  vocab_only stops after the
+// vocabulary.  Throws lvk::Error.
+void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_t s,
+                void (*progress)(float, void *), void * progress_ud);
+
+}  // namespace lvk

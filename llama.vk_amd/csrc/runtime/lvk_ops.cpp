@@ -1,0 +1,181 @@
+// lvk_ops.cpp -- operator-level C ABI (include/lvk_ops.h): each op runs the
+// production kernel on host buffers so tests can pin it against the oracle.
+#include <immintrin.h>
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../../include/llama.h"
+#include "../../../include/lvk_ops.h"
+#include "lvk_context.h"
+
+namespace {
+
+struct Dev {
+    std::vector<void *> ptrs;
+    void * get(size_t n) {
+        void * p = nullptr;
+        LVK_HIP(hipMalloc(&p, n ? n : 16));
+        ptrs.push_back(p);
+        return p;
+    }
+    template <class T> T * up(const T * h, size_t n) {
+        T * d = (T *) get(n * sizeof(T));
+        LVK_HIP(hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
+        return d;
+    }
+    ~Dev() { for (void * p : ptrs) (void) hipFree(p); }
+};
+
+int fail(const char * fn, const std::string & m) {
+    fprintf(stderr, "%s: %s\n", fn, m.c_str());
+    return -1;
+}
+
+size_t block_bytes(int type) { return type == lvk::Q4_0 ? 20 : 24; }
+
+__attribute__((target("f16c"))) uint16_t h_f32_to_f16(float f) { return _cvtss_sh(f, 0); }
+
+}  // namespace
+
+extern "C" {
+
+int lvk_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char * lvk_version(void) { return "llama.vk_amd 0.1 (gfx950)"; }
+
+int lvk_quantize_rows(int type, const float * x, int n, int k, void * y) {
+    try {
+        if (k % 32) return fail(__func__, "k must be a multiple of 32");
+        Dev dv;
+        const size_t nb = (size_t) k / 32;
+        float * xd = dv.up(x, (size_t) n * k);
+        lvk::ActQ q;
+        q.nb = (int) nb;
+        q.d = (float *) dv.get((size_t) n * nb * 4);
+        q.m = (float *) dv.get((size_t) n * nb * 4);
+        q.qs = (uint4 *) dv.get((size_t) n * nb * 16);
+        LVK_HIP(lvk::launch_quantize_act(xd, n, k, type, q, nullptr));
+        std::vector<float> d((size_t) n * nb), m((size_t) n * nb);
+        std::vector<uint8_t> qs((size_t) n * nb * 16);
+        LVK_HIP(hipMemcpy(d.data(), q.d, d.size() * 4, hipMemcpyDeviceToHost));
+        LVK_HIP(hipMemcpy(m.data(), q.m, m.size() * 4, hipMemcpyDeviceToHost));
+        LVK_HIP(hipMemcpy(qs.data(), q.qs, qs.size(), hipMemcpyDeviceToHost));
+        uint8_t * out = (uint8_t *) y;
+        const size_t bb = block_bytes(type);
+        for (size_t i = 0; i < (size_t) n * nb; ++i) {
+            std::memcpy(out + i * bb, &d[i], 4);
+            if (type == lvk::Q4_1) std::memcpy(out + i * bb + 4, &m[i], 4);
+            std::memcpy(out + i * bb + bb - 16, &qs[i * 16], 16);
+        }
+        return 0;
+    } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
+static int mul_mat_impl(int type, const void * w, int m, int k, const float * g, const float * x, int n, float * y,
+                        bool norm) {
+    if (m % 16 || k % 256) return fail("lvk_mul_mat_q", "need m % 16 == 0 and k % 256 == 0");
+    Dev dv;
+    const size_t nb = (size_t) k / 32, bb = block_bytes(type);
+    void * wd = dv.up((const uint8_t *) w, (size_t) m * nb * bb);
+    lvk::QMatrix q;
+    q.qtype = type; q.M = m; q.K = k;
+    q.nib = (const uint4 *) dv.get((size_t) m * nb * 16);
+    q.scl = dv.get((size_t) m * nb * (type == lvk::Q4_0 ? 4 : 8));
+    LVK_HIP(lvk::launch_repack(wd, type, m, k, (uint4 *) q.nib, (void *) q.scl, nullptr));
+    lvk::StepParams sp{0, n, 0, 0};
+    lvk::StepParams * spd = dv.up(&sp, 1);
+    float * yd = (float *) dv.get((size_t) n * m * 4);
+    lvk::MvLaunch L;
+    L.w = q; L.sp = spd; L.n_tokens = n; L.y = yd;
+    float * xd = dv.up(x, (size_t) n * k);
+    if (norm) {
+        L.x = xd;
+        L.g = dv.up(g, (size_t) k);
+        LVK_HIP(lvk::launch_matvec(L, lvk::PRO_NORM, lvk::EPI_STORE, nullptr));
+    } else {
+        lvk::ActQ a;
+        a.nb = (int) nb;
+        a.d = (float *) dv.get((size_t) n * nb * 4);
+        a.m = (float *) dv.get((size_t) n * nb * 4);
+        a.qs = (uint4 *) dv.get((size_t) n * nb * 16);
+        LVK_HIP(lvk::launch_quantize_act(xd, n, k, type, a, nullptr));
+        L.xq = a;
+        LVK_HIP(lvk::launch_matvec(L, lvk::PRO_ACTQ, lvk::EPI_STORE, nullptr));
+    }
+    LVK_HIP(hipMemcpy(y, yd, (size_t) n * m * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int lvk_mul_mat_q(int type, const void * w, int m, int k, const float * x, int n, float * y) {
+    try { return mul_mat_impl(type, w, m, k, nullptr, x, n, y, false); }
+    catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
+int lvk_mul_mat_q_norm(int type, const void * w, int m, int k, const float * g, const float * x, int n, float * y) {
+    try { return mul_mat_impl(type, w, m, k, g, x, n, y, true); }
+    catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
+int lvk_attention(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head, int n_ctx,
+                  int n_past, int n, float * out) {
+    try {
+        Dev dv;
+        const size_t CE = (size_t) n_ctx * n_embd;
+        std::vector<uint16_t> q16((size_t) n * n_embd);
+        for (size_t i = 0; i < q16.size(); ++i) q16[i] = h_f32_to_f16(q[i]);   // ggml.c:6420-6433
+        lvk::StepParams sp{n_past, n, 0, 0};
+        lvk::AttnLaunch A{};
+        A.q16 = dv.up(q16.data(), q16.size());
+        A.kc = dv.up(kc, CE);
+        A.vc = dv.up(vc, CE);
+        A.scores = (float *) dv.get((size_t) n * n_head * n_ctx * 4);
+        A.out.nb = n_embd / 32;
+        A.out.d = (float *) dv.get((size_t) n * n_embd / 32 * 4);
+        A.out.m = (float *) dv.get((size_t) n * n_embd / 32 * 4);
+        A.out.qs = (uint4 *) dv.get((size_t) n * n_embd / 32 * 16);
+        A.out_qtype = lvk::Q4_0;
+        std::vector<uint16_t> te, ts;
+        lvk::host_fp16_tables(te, ts);
+        A.exp_tab = dv.up(te.data(), te.size());
+        A.sp = dv.up(&sp, 1);
+        A.n_tokens = n; A.n_embd = n_embd; A.n_head = n_head; A.n_ctx = n_ctx;
+        float * od = (float *) dv.get((size_t) n * n_embd * 4);
+        A.out_f32 = od;
+        LVK_HIP(lvk::launch_attention(A, nullptr));
+        LVK_HIP(hipMemcpy(out, od, (size_t) n * n_embd * 4, hipMemcpyDeviceToHost));
+        return 0;
+    } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
+int lvk_rms_norm_mul(const float * x, const float * g, int k, int n, float * y) {
+    try {
+        Dev dv;
+        float * xd = dv.up(x, (size_t) n * k);
+        float * gd = dv.up(g, (size_t) k);
+        float * yd = (float *) dv.get((size_t) n * k * 4);
+        LVK_HIP(lvk::launch_rmsnorm_rows(xd, gd, k, n, yd, nullptr));
+        LVK_HIP(hipMemcpy(y, yd, (size_t) n * k * 4, hipMemcpyDeviceToHost));
+        return 0;
+    } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
+void lvk_set_profiling(struct llama_context * ctx, int on) { ctx->c.profiling = on != 0; }
+void lvk_reset_profile(struct llama_context * ctx) { ctx->c.prof = lvk::Profile{}; }
+int lvk_get_profile(struct llama_context * ctx, double * ms, long * launches, double * bytes, int n) {
+    for (int i = 0; i < n && i < lvk::K_NCLASS; ++i) {
+        ms[i] = ctx->c.prof.ms[i];
+        launches[i] = ctx->c.prof.launches[i];
+        bytes[i] = ctx->c.prof.bytes[i];
+    }
+    return lvk::K_NCLASS;
+}
+size_t lvk_weight_bytes(struct llama_context * ctx) { return ctx->c.model.weight_bytes; }
+void lvk_set_graph(struct llama_context * ctx, int on) { ctx->c.use_graph = on != 0; }
+
+}  // extern "C"

@@ -1,0 +1,245 @@
+"""Python host mirror of the llama.vk_amd C ABI (include/llama.h, include/lvk_ops.h).
+
+A thin ctypes layer over lib/libllama_vk_amd.so, mirroring the reference
+llama.h surface (same function names and argument meaning) for tests and
+bench.py.  There is no fallback: if the shared library is missing or fails to
+load, importing this module raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libllama_vk_amd.so")
+GEN_BIN = os.path.join(HERE, "bin", "lvk-gen-model")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError("llama.vk_amd: %s not built (run __graft_entry__.build() or make -C llama.vk_amd)" % LIB_PATH)
+lib = C.CDLL(LIB_PATH)
+
+f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+u16p = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
+u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+
+PROGRESS_CB = C.CFUNCTYPE(None, C.c_float, C.c_void_p)
+
+
+class llama_context_params(C.Structure):
+    """reference llama.h:49-66, field for field"""
+    _fields_ = [
+        ("n_ctx", C.c_int),
+        ("n_parts", C.c_int),
+        ("seed", C.c_int),
+        ("f16_kv", C.c_bool),
+        ("logits_all", C.c_bool),
+        ("vocab_only", C.c_bool),
+        ("use_mmap", C.c_bool),
+        ("use_mlock", C.c_bool),
+        ("embedding", C.c_bool),
+        ("progress_callback", PROGRESS_CB),
+        ("progress_callback_user_data", C.c_void_p),
+    ]
+
+
+def _sig(name, res, args):
+    fn = getattr(lib, name)
+    fn.restype = res
+    fn.argtypes = args
+    return fn
+
+
+# llama.h
+_sig("llama_context_default_params", llama_context_params, [])
+_sig("llama_mmap_supported", C.c_bool, [])
+_sig("llama_mlock_supported", C.c_bool, [])
+_sig("llama_init_from_file", C.c_void_p, [C.c_char_p, llama_context_params])
+_sig("llama_free", None, [C.c_void_p])
+_sig("llama_model_quantize", C.c_int, [C.c_char_p, C.c_char_p, C.c_int])
+_sig("llama_get_kv_cache", C.POINTER(C.c_uint8), [C.c_void_p])
+_sig("llama_get_kv_cache_size", C.c_size_t, [C.c_void_p])
+_sig("llama_get_kv_cache_token_count", C.c_int, [C.c_void_p])
+_sig("llama_set_kv_cache", None, [C.c_void_p, u8p, C.c_size_t, C.c_int])
+_sig("llama_eval", C.c_int, [C.c_void_p, i32p, C.c_int, C.c_int, C.c_int])
+_sig("llama_tokenize", C.c_int, [C.c_void_p, C.c_char_p, i32p, C.c_int, C.c_bool])
+_sig("llama_n_vocab", C.c_int, [C.c_void_p])
+_sig("llama_n_ctx", C.c_int, [C.c_void_p])
+_sig("llama_n_embd", C.c_int, [C.c_void_p])
+_sig("llama_get_logits", C.POINTER(C.c_float), [C.c_void_p])
+_sig("llama_get_embeddings", C.POINTER(C.c_float), [C.c_void_p])
+_sig("llama_token_to_str", C.c_char_p, [C.c_void_p, C.c_int])
+_sig("llama_token_bos", C.c_int, [])
+_sig("llama_token_eos", C.c_int, [])
+_sig("llama_sample_top_p_top_k", C.c_int, [C.c_void_p, i32p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float])
+_sig("llama_print_timings", None, [C.c_void_p])
+_sig("llama_reset_timings", None, [C.c_void_p])
+_sig("llama_print_system_info", C.c_char_p, [])
+# lvk_ops.h
+_sig("lvk_device_count", C.c_int, [])
+_sig("lvk_version", C.c_char_p, [])
+_sig("lvk_quantize_rows", C.c_int, [C.c_int, f32p, C.c_int, C.c_int, u8p])
+_sig("lvk_mul_mat_q", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, f32p, C.c_int, f32p])
+_sig("lvk_mul_mat_q_norm", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, f32p, f32p, C.c_int, f32p])
+_sig("lvk_attention", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p])
+_sig("lvk_rms_norm_mul", C.c_int, [f32p, f32p, C.c_int, C.c_int, f32p])
+_sig("lvk_set_profiling", None, [C.c_void_p, C.c_int])
+_sig("lvk_get_profile", C.c_int, [C.c_void_p, f64p, i64p, f64p, C.c_int])
+_sig("lvk_reset_profile", None, [C.c_void_p])
+_sig("lvk_weight_bytes", C.c_size_t, [C.c_void_p])
+_sig("lvk_set_graph", None, [C.c_void_p, C.c_int])
+
+BLOCK_BYTES = {2: 20, 3: 24}
+KCLASS = ["embed", "qkv", "attention", "wo", "w13", "w2", "lm_head"]
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError("%s failed (rc=%d)" % (what, rc))
+
+
+class Llama:
+    """One llama_context (reference llama.h API, GPU forward pass)."""
+
+    def __init__(self, path, n_ctx=512, seed=1, logits_all=False, embedding=False, vocab_only=False, f16_kv=True):
+        p = lib.llama_context_default_params()
+        p.n_ctx = n_ctx
+        p.seed = seed
+        p.f16_kv = f16_kv
+        p.logits_all = logits_all
+        p.embedding = embedding
+        p.vocab_only = vocab_only
+        self._cb = PROGRESS_CB(lambda prog, ud: None)
+        p.progress_callback = self._cb
+        self.ctx = lib.llama_init_from_file(path.encode(), p)
+        if not self.ctx:
+            raise RuntimeError("llama_init_from_file failed for %s" % path)
+        self.logits_all = logits_all
+        self.n_vocab = lib.llama_n_vocab(self.ctx)
+        self.n_embd = lib.llama_n_embd(self.ctx)
+        self.n_ctx = lib.llama_n_ctx(self.ctx)
+        self._last_n = 1
+
+    def eval(self, tokens, n_past, n_threads=1):
+        t = np.ascontiguousarray(tokens, np.int32)
+        _check(lib.llama_eval(self.ctx, t, len(t), n_past, n_threads), "llama_eval")
+        self._last_n = len(t)
+        return self.logits()
+
+    def logits(self):
+        rows = self._last_n if self.logits_all else 1
+        ptr = lib.llama_get_logits(self.ctx)
+        return np.ctypeslib.as_array(ptr, shape=(rows * self.n_vocab,)).reshape(rows, self.n_vocab).copy()
+
+    def embeddings(self):
+        return np.ctypeslib.as_array(lib.llama_get_embeddings(self.ctx), shape=(self.n_embd,)).copy()
+
+    def tokenize(self, text, add_bos=True):
+        buf = np.zeros(len(text.encode()) + 8, np.int32)
+        n = lib.llama_tokenize(self.ctx, text.encode(), buf, len(buf), add_bos)
+        if n < 0:
+            raise RuntimeError("llama_tokenize: too many tokens")
+        return buf[:n].copy()
+
+    def token_to_str(self, tok):
+        return lib.llama_token_to_str(self.ctx, tok)
+
+    def sample(self, last_tokens, top_k=40, top_p=0.95, temp=0.8, repeat_penalty=1.1):
+        lt = np.ascontiguousarray(last_tokens, np.int32)
+        return lib.llama_sample_top_p_top_k(self.ctx, lt, len(lt), top_k, top_p, temp, repeat_penalty)
+
+    def kv_cache(self):
+        n = lib.llama_get_kv_cache_size(self.ctx)
+        return np.ctypeslib.as_array(lib.llama_get_kv_cache(self.ctx), shape=(n,)).copy()
+
+    def set_kv_cache(self, buf, n_tokens):
+        buf = np.ascontiguousarray(buf, np.uint8)
+        lib.llama_set_kv_cache(self.ctx, buf, buf.size, n_tokens)
+
+    def set_profiling(self, on):
+        lib.lvk_set_profiling(self.ctx, int(on))
+
+    def set_graph(self, on):
+        lib.lvk_set_graph(self.ctx, int(on))
+
+    def reset_profile(self):
+        lib.lvk_reset_profile(self.ctx)
+
+    def profile(self):
+        ms = np.zeros(8, np.float64)
+        la = np.zeros(8, np.int64)
+        by = np.zeros(8, np.float64)
+        n = lib.lvk_get_profile(self.ctx, ms, la, by, 8)
+        return {KCLASS[i]: {"ms": float(ms[i]), "launches": int(la[i]), "bytes": float(by[i])} for i in range(n)}
+
+    def weight_bytes(self):
+        return int(lib.lvk_weight_bytes(self.ctx))
+
+    def print_timings(self):
+        lib.llama_print_timings(self.ctx)
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            lib.llama_free(self.ctx)
+            self.ctx = None
+
+    __del__ = close
+
+
+# ---------------------------------------------------------------- operator level
+def quantize_rows(x, qtype):
+    x = np.ascontiguousarray(x, np.float32)
+    n, k = x.shape
+    y = np.zeros(n * (k // 32) * BLOCK_BYTES[qtype], np.uint8)
+    _check(lib.lvk_quantize_rows(qtype, x, n, k, y), "lvk_quantize_rows")
+    return y.reshape(n, -1)
+
+
+def mul_mat_q(qtype, w_rows, m, k, x):
+    x = np.ascontiguousarray(x, np.float32)
+    n = x.shape[0]
+    y = np.zeros(n * m, np.float32)
+    _check(lib.lvk_mul_mat_q(qtype, np.ascontiguousarray(w_rows, np.uint8).ravel(), m, k, x, n, y), "lvk_mul_mat_q")
+    return y.reshape(n, m)
+
+
+def mul_mat_q_norm(qtype, w_rows, m, k, g, x):
+    x = np.ascontiguousarray(x, np.float32)
+    n = x.shape[0]
+    y = np.zeros(n * m, np.float32)
+    _check(lib.lvk_mul_mat_q_norm(qtype, np.ascontiguousarray(w_rows, np.uint8).ravel(), m, k,
+                                  np.ascontiguousarray(g, np.float32), x, n, y), "lvk_mul_mat_q_norm")
+    return y.reshape(n, m)
+
+
+def attention(kc, vc, q, n_embd, n_head, n_ctx, n_past, n):
+    out = np.zeros(n * n_embd, np.float32)
+    _check(lib.lvk_attention(np.ascontiguousarray(kc, np.uint16), np.ascontiguousarray(vc, np.uint16),
+                             np.ascontiguousarray(q, np.float32).ravel(), n_embd, n_head, n_ctx, n_past, n, out),
+           "lvk_attention")
+    return out
+
+
+def rms_norm_mul(x, g):
+    x = np.ascontiguousarray(x, np.float32)
+    n, k = x.shape
+    y = np.zeros_like(x)
+    _check(lib.lvk_rms_norm_mul(x, np.ascontiguousarray(g, np.float32), k, n, y), "lvk_rms_norm_mul")
+    return y
+
+
+def device_count():
+    return lib.lvk_device_count()
+
+
+def gen_model(path, n_embd=4096, n_head=32, n_layer=32, ftype=2, seed=1, n_vocab=32000, n_mult=256, vocab=None):
+    """Write a seeded synthetic ggjt model with the bundled generator."""
+    import subprocess
+    cmd = [GEN_BIN, path, "--n-embd", str(n_embd), "--n-head", str(n_head), "--n-layer", str(n_layer),
+           "--ftype", str(ftype), "--seed", str(seed), "--n-vocab", str(n_vocab), "--n-mult", str(n_mult)]
+    if vocab:
+        cmd += ["--vocab", vocab]
+    subprocess.check_call(cmd, stderr=subprocess.DEVNULL)
+    return path

@@ -1,0 +1,63 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "llama.vk_amd"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+def _ensure_built():
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "oracle"], stdout=subprocess.DEVNULL)
+    if not os.path.exists(os.path.join(ROOT, "llama.vk_amd", "bin", "lvk-gen-model")):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "llama.vk_amd"),
+                               os.path.join(ROOT, "llama.vk_amd", "bin", "lvk-gen-model")], stdout=subprocess.DEVNULL)
+
+
+@pytest.fixture(scope="session")
+def model_dir(tmp_path_factory):
+    _ensure_built()
+    return str(tmp_path_factory.mktemp("models"))
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    _ensure_built()
+    from oracle_lib import Oracle
+    return Oracle()
+
+
+@pytest.fixture(scope="session")
+def ref():
+    from oracle_lib import REF_SO, Ref
+    if not os.path.exists(REF_SO):
+        pytest.skip("reference build oracle/_ref/libref.so not present")
+    return Ref()
+
+
+TINY = {
+    "tiny_q4_0": dict(n_embd=256, n_head=2, n_layer=32, ftype=2, seed=1),
+    "tiny_q4_1": dict(n_embd=256, n_head=2, n_layer=40, ftype=3, seed=7),
+}
+
+
+@pytest.fixture(scope="session")
+def tiny_models(model_dir):
+    from oracle_lib import gen_model
+    return {k: gen_model(os.path.join(model_dir, k + ".bin"), **v) for k, v in TINY.items()}
+
+
+@pytest.fixture(scope="session")
+def gpu_available():
+    import lvk
+    if lvk.device_count() < 1:
+        pytest.fail("no GPU visible to the gpu-marked test (HIP extension loaded, but no device)")
+    return True

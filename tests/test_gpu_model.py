@@ -1,0 +1,97 @@
+"""Whole-model parity through the drop-in llama.h API on the GPU.
+
+The tiny seeded models are evaluated with the reference's chunking (prompt
+batches then single-token decode, SURVEY.md finding 7) and compared
+bit-for-bit with (a) the golden logits produced by the reference build and
+(b) the CPU oracle on the same inputs.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def lvk(gpu_available):
+    import lvk as m
+    return m
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_tiny_q4_0_matches_reference_golden(lvk, tiny_models, graph):
+    g = np.load(os.path.join(GOLD, "tiny_q4_0.npz"), allow_pickle=False)
+    m = lvk.Llama(tiny_models["tiny_q4_0"], n_ctx=512)
+    m.set_graph(graph)
+    n_past, off = 0, 0
+    for step, n in enumerate(g["chunks"]):
+        lg = m.eval(g["tokens"][off:off + n], n_past)
+        assert np.array_equal(bits(lg[-1]), bits(g["logits"][step])), "step %d (n=%d, n_past=%d)" % (step, n, n_past)
+        n_past += n
+        off += n
+    m.close()
+
+
+def test_tiny_q4_0_long_decode_vs_oracle(lvk, oracle, tiny_models):
+    path = tiny_models["tiny_q4_0"]
+    m = lvk.Llama(path, n_ctx=256)
+    om = oracle.model(path, 256)
+    toks = np.array([1, 450, 4996, 17354, 1701, 29916], np.int32)
+    a = m.eval(toks, 0)
+    b = om.eval(toks, 0)
+    assert np.array_equal(bits(a), bits(b))
+    n_past = len(toks)
+    tok = int(np.argmax(a[-1]))
+    for _ in range(70):          # crosses the 32/64-position f16-dot tail boundaries
+        a = m.eval([tok], n_past)
+        b = om.eval([tok], n_past)
+        assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past
+        n_past += 1
+        tok = int(np.argmax(a[-1]))
+    m.close()
+    om.close()
+
+
+def test_logits_all_and_embeddings(lvk, oracle, tiny_models):
+    path = tiny_models["tiny_q4_0"]
+    m = lvk.Llama(path, n_ctx=128, logits_all=True, embedding=True)
+    om = oracle.model(path, 128)
+    toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 40)], np.int32)
+    a = m.eval(toks, 0)
+    b = om.eval(toks, 0, logits_all=True)
+    assert a.shape == (40, m.n_vocab)
+    assert np.array_equal(bits(a), bits(b))
+    e = m.embeddings()
+    assert e.shape == (m.n_embd,) and np.isfinite(e).all()
+    m.close()
+    om.close()
+
+
+def test_kv_cache_roundtrip(lvk, tiny_models):
+    path = tiny_models["tiny_q4_0"]
+    m = lvk.Llama(path, n_ctx=128)
+    toks = np.arange(1, 20, dtype=np.int32)
+    m.eval(toks, 0)
+    kv = m.kv_cache()
+    a = m.eval([42], 19)
+    m2 = lvk.Llama(path, n_ctx=128)
+    m2.set_kv_cache(kv, 19)
+    b = m2.eval([42], 19)
+    assert np.array_equal(bits(a), bits(b))
+    m.close()
+    m2.close()
+
+
+def test_eval_errors(lvk, tiny_models):
+    m = lvk.Llama(tiny_models["tiny_q4_0"], n_ctx=64)
+    with pytest.raises(RuntimeError):
+        m.eval(np.arange(1, 70, dtype=np.int32), 0)     # exceeds n_ctx -> llama_eval returns 1
+    with pytest.raises(RuntimeError):
+        m.eval([40000], 0)                              # token id out of range
+    m.close()

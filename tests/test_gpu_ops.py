@@ -1,0 +1,88 @@
+"""Operator-level parity of the HIP kernels against the CPU oracle (bit-exact).
+
+Each op runs the production kernel through include/lvk_ops.h on seeded
+inputs; the oracle restates the reference AVX2 arithmetic (pinned by
+test_oracle_golden.py against the reference's own outputs).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def lvk(gpu_available):
+    import lvk as m
+    return m
+
+
+@pytest.mark.parametrize("k", [256, 4096, 11008])
+def test_quantize_rows_q4_0(lvk, oracle, k):
+    rng = np.random.default_rng(k)
+    x = np.concatenate([rng.standard_normal((4, k)) * s for s in (1e-3, 1.0, 50.0)]).astype(np.float32)
+    x[0, :32] = 0.0          # an all-zero block (id = 0 branch)
+    x[1, 5] = 1e-30          # tiny values
+    got = lvk.quantize_rows(x, 2)
+    for i, row in enumerate(x):
+        assert np.array_equal(got[i], oracle.quantize(row, 2)), "row %d" % i
+
+
+def _weights(oracle, rng, m, k, qt, scale=0.02):
+    w = (rng.standard_normal((m, k)) * scale).astype(np.float32)
+    return np.stack([oracle.quantize(r, qt, reference=True) for r in w])
+
+
+def _oracle_mm(oracle, wq, xq_rows, k, qt):
+    return np.array([[oracle.vec_dot(qt, k, wr, xr) for wr in wq] for xr in xq_rows], np.float32)
+
+
+@pytest.mark.parametrize("m,k,n", [(64, 256, 1), (48, 4096, 1), (32, 11008, 1), (64, 4096, 5), (16, 4096, 9)])
+def test_mul_mat_q4_0(lvk, oracle, m, k, n):
+    rng = np.random.default_rng(m * 7 + k + n)
+    wq = _weights(oracle, rng, m, k, 2)
+    x = (rng.standard_normal((n, k)) * 1.3).astype(np.float32)
+    got = lvk.mul_mat_q(2, wq, m, k, x)
+    want = _oracle_mm(oracle, wq, [oracle.quantize(r, 2) for r in x], k, 2)
+    assert np.array_equal(bits(got), bits(want))
+
+
+@pytest.mark.parametrize("m,k,n", [(64, 256, 1), (64, 4096, 1), (64, 4096, 6), (128, 8192, 1)])
+def test_mul_mat_q4_0_rmsnorm_prologue(lvk, oracle, m, k, n):
+    rng = np.random.default_rng(m + k * 3 + n)
+    wq = _weights(oracle, rng, m, k, 2)
+    x = (rng.standard_normal((n, k)) * 2.0).astype(np.float32)
+    g = (1.0 + 0.1 * rng.standard_normal(k)).astype(np.float32)
+    got = lvk.mul_mat_q_norm(2, wq, m, k, g, x)
+    xn = np.zeros_like(x)
+    oracle.lib.orc_rms_norm(x, k, n, xn)
+    xn = (g[None, :] * xn).astype(np.float32)
+    want = _oracle_mm(oracle, wq, [oracle.quantize(r, 2) for r in xn], k, 2)
+    assert np.array_equal(bits(got), bits(want))
+
+
+@pytest.mark.parametrize("n_past,N", [(0, 1), (5, 1), (31, 1), (32, 1), (200, 1), (40, 3), (60, 37), (0, 64), (10, 100)])
+def test_attention(lvk, oracle, n_past, N):
+    E, H, C = 512, 4, 256
+    rng = np.random.default_rng(n_past * 131 + N)
+    kc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
+    vc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
+    q = rng.standard_normal(N * E).astype(np.float32)
+    got = lvk.attention(kc, vc, q, E, H, C, n_past, N)
+    want = np.zeros(N * E, np.float32)
+    oracle.lib.orc_attention(kc, vc, q, E, H, C, n_past, N, want)
+    assert np.array_equal(bits(got), bits(want))
+
+
+def test_rms_norm_mul(lvk, oracle):
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal((4, 4096)) * 3).astype(np.float32)
+    g = (1 + 0.1 * rng.standard_normal(4096)).astype(np.float32)
+    got = lvk.rms_norm_mul(x, g)
+    want = np.zeros_like(x)
+    oracle.lib.orc_rms_norm(x, 4096, 4, want)
+    want = (g[None, :] * want).astype(np.float32)
+    assert np.array_equal(bits(got), bits(want))
