@@ -44,8 +44,16 @@ LVK_API int lvk_mul_mat_q_norm(int type, const void * w, int m, int k, const flo
 LVK_API int lvk_attention(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
                           int n_ctx, int n_past, int n, float * out);
 
+/* lvk_attention plus the pre-softmax scores [n][n_head][n_ctx] (scaled, -inf where masked), followed in
+ * scores_out by the f16 probabilities [n][n_head][n_ctx] (so scores_out holds 1.5x that many floats) */
+LVK_API int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
+                                 int n_ctx, int n_past, int n, float * out, float * scores_out);
+
 /* y[t] = g * rms_norm(x[t]) (ggml.c:6024-6080 + llama.cpp:984) */
 LVK_API int lvk_rms_norm_mul(const float * x, const float * g, int k, int n, float * y);
+
+/* the 64Ki-entry fp16 exp / silu tables the library uploads (ggml.c:2915-2927) */
+LVK_API void lvk_host_tables(uint16_t * exp_tab, uint16_t * silu_tab);
 
 /* decode-step profiling of a llama_context: when enabled, every eval records
  * HIP events around each kernel class (0 embed, 1 qkv, 2 attention, 3 wo,

@@ -89,7 +89,7 @@ template <int QT>
 __global__ __launch_bounds__(128) void k_attn_pv(const float * __restrict__ scores, const uint16_t * __restrict__ vc,
                                                  const uint16_t * __restrict__ exp_tab, ActQ out,
                                                  const StepParams * sp, int E, int hd, int n_ctx,
-                                                 float * __restrict__ out_f32) {
+                                                 float * __restrict__ out_f32, uint16_t * __restrict__ p16_out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int n_past = sp->n_past, N = sp->n_tokens;
     const int n_kv = n_past + N;
@@ -127,6 +127,8 @@ __global__ __launch_bounds__(128) void k_attn_pv(const float * __restrict__ scor
     const int n_pad = (n_kv + 31) & ~31;
     for (int p = tid; p < n_pad; p += 128) p16[p] = p < n_kv ? f32_to_f16(ev[p] * sc) : (uint16_t) 0;
     __syncthreads();
+    if (p16_out && dc == 0)
+        for (int p = tid; p < n_kv; p += 128) p16_out[((size_t) t * gridDim.y + h) * n_ctx + p] = p16[p];
 
     // KQV: ggml_vec_dot_f16(n_kv, V row, P)
     const int d = dc * 32 + (tid >> 2);
@@ -194,7 +196,7 @@ hipError_t launch_attention(const AttnLaunch & A, hipStream_t s) {
     dim3 g2(hd / 32, A.n_head, A.n_tokens);
     const size_t lds = (size_t) A.n_ctx * 6 + 64 + 256;
     hipLaunchKernelGGL(k_attn_pv<Q4_0>, g2, dim3(128), lds, s, A.scores, A.vc, A.exp_tab, A.out, A.sp,
-                       A.n_embd, hd, A.n_ctx, A.out_f32);
+                       A.n_embd, hd, A.n_ctx, A.out_f32, A.p16_out);
     return hipGetLastError();
 }
 

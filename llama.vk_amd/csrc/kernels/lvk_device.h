@@ -14,9 +14,14 @@ namespace lvk {
 constexpr int QK = 32;    // elements per quant block (ggml.c:416)
 constexpr int WAVE = 64;  // CDNA wavefront
 
+// f32 -> f16 RNE as an opaque instruction: a plain (_Float16) cast lets the
+// backend fold a preceding f32 mul/add into v_fma_mixlo_f16, which rounds the
+// exact product straight to f16 (one rounding instead of the reference's two:
+// f32 result, then _cvtss_sh) -- observed on ROCm 7.2 in the softmax P->f16.
 __device__ __forceinline__ uint16_t f32_to_f16(float x) {
-    _Float16 h = (_Float16) x;   // v_cvt_f16_f32, round-to-nearest-even
-    return __builtin_bit_cast(uint16_t, h);
+    uint32_t r;
+    asm volatile("v_cvt_f16_f32 %0, %1" : "=v"(r) : "v"(x));
+    return (uint16_t) r;
 }
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
     return (float) __builtin_bit_cast(_Float16, h);   // exact

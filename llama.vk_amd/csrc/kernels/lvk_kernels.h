@@ -94,6 +94,7 @@ struct AttnLaunch {
     const StepParams * sp;
     int n_tokens, n_embd, n_head, n_ctx;
     float * out_f32 = nullptr; // optional: also store the unquantized merged heads [N][E]
+    uint16_t * p16_out = nullptr; // optional (debug): f16 probabilities [N][H][n_ctx]
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
 

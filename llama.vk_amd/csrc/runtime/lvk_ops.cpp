@@ -122,8 +122,15 @@ int lvk_mul_mat_q_norm(int type, const void * w, int m, int k, const float * g, 
     catch (const lvk::Error & e) { return fail(__func__, e.msg); }
 }
 
+int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
+                         int n_ctx, int n_past, int n, float * out, float * scores_out);
 int lvk_attention(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head, int n_ctx,
                   int n_past, int n, float * out) {
+    return lvk_attention_scores(kc, vc, q, n_embd, n_head, n_ctx, n_past, n, out, nullptr);
+}
+
+int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
+                         int n_ctx, int n_past, int n, float * out, float * scores_out) {
     try {
         Dev dv;
         const size_t CE = (size_t) n_ctx * n_embd;
@@ -147,8 +154,17 @@ int lvk_attention(const uint16_t * kc, const uint16_t * vc, const float * q, int
         A.n_tokens = n; A.n_embd = n_embd; A.n_head = n_head; A.n_ctx = n_ctx;
         float * od = (float *) dv.get((size_t) n * n_embd * 4);
         A.out_f32 = od;
+        uint16_t * pd = nullptr;
+        if (scores_out) pd = (uint16_t *) dv.get((size_t) n * n_head * n_ctx * 2);
+        A.p16_out = pd;
         LVK_HIP(lvk::launch_attention(A, nullptr));
         LVK_HIP(hipMemcpy(out, od, (size_t) n * n_embd * 4, hipMemcpyDeviceToHost));
+        if (scores_out) {
+            LVK_HIP(hipMemcpy(scores_out, A.scores, (size_t) n * n_head * n_ctx * 4, hipMemcpyDeviceToHost));
+            // debug: the f16 probabilities overwrite the second half of scores_out's bytes? no -- appended
+            LVK_HIP(hipMemcpy(scores_out + (size_t) n * n_head * n_ctx, pd, (size_t) n * n_head * n_ctx * 2,
+                              hipMemcpyDeviceToHost));
+        }
         return 0;
     } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
 }
@@ -163,6 +179,13 @@ int lvk_rms_norm_mul(const float * x, const float * g, int k, int n, float * y) 
         LVK_HIP(hipMemcpy(y, yd, (size_t) n * k * 4, hipMemcpyDeviceToHost));
         return 0;
     } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
+void lvk_host_tables(uint16_t * exp_tab, uint16_t * silu_tab) {
+    std::vector<uint16_t> te, ts;
+    lvk::host_fp16_tables(te, ts);
+    std::memcpy(exp_tab, te.data(), 65536 * 2);
+    std::memcpy(silu_tab, ts.data(), 65536 * 2);
 }
 
 void lvk_set_profiling(struct llama_context * ctx, int on) { ctx->c.profiling = on != 0; }

@@ -84,7 +84,9 @@ _sig("lvk_quantize_rows", C.c_int, [C.c_int, f32p, C.c_int, C.c_int, u8p])
 _sig("lvk_mul_mat_q", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, f32p, C.c_int, f32p])
 _sig("lvk_mul_mat_q_norm", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, f32p, f32p, C.c_int, f32p])
 _sig("lvk_attention", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p])
+_sig("lvk_attention_scores", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p, f32p])
 _sig("lvk_rms_norm_mul", C.c_int, [f32p, f32p, C.c_int, C.c_int, f32p])
+_sig("lvk_host_tables", None, [u16p, u16p])
 _sig("lvk_set_profiling", None, [C.c_void_p, C.c_int])
 _sig("lvk_get_profile", C.c_int, [C.c_void_p, f64p, i64p, f64p, C.c_int])
 _sig("lvk_reset_profile", None, [C.c_void_p])
@@ -222,12 +224,30 @@ def attention(kc, vc, q, n_embd, n_head, n_ctx, n_past, n):
     return out
 
 
+def attention_scores(kc, vc, q, n_embd, n_head, n_ctx, n_past, n):
+    out = np.zeros(n * n_embd, np.float32)
+    m = n * n_head * n_ctx
+    sc = np.zeros(m + (m + 1) // 2, np.float32)
+    _check(lib.lvk_attention_scores(np.ascontiguousarray(kc, np.uint16), np.ascontiguousarray(vc, np.uint16),
+                                    np.ascontiguousarray(q, np.float32).ravel(), n_embd, n_head, n_ctx, n_past, n,
+                                    out, sc), "lvk_attention_scores")
+    p16 = sc[m:].view(np.uint16)[:m].reshape(n, n_head, n_ctx)
+    return out, sc[:m].reshape(n, n_head, n_ctx), p16
+
+
 def rms_norm_mul(x, g):
     x = np.ascontiguousarray(x, np.float32)
     n, k = x.shape
     y = np.zeros_like(x)
     _check(lib.lvk_rms_norm_mul(x, np.ascontiguousarray(g, np.float32), k, n, y), "lvk_rms_norm_mul")
     return y
+
+
+def host_tables():
+    e = np.zeros(65536, np.uint16)
+    s = np.zeros(65536, np.uint16)
+    lib.lvk_host_tables(e, s)
+    return e, s
 
 
 def device_count():
