@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""bench.py -- LLaMA-7B Q4_0 single-stream decode on MI355X (BASELINE.json configs[1]).
+
+A step = one llama_eval of one token (the reference main's greedy loop:
+llama_eval -> argmax of the returned logits -> next token), on a seeded
+synthetic 7B Q4_0 ggjt file (no checkpoints exist here).  Workload: 16-token
+prompt, then greedy decode over positions 16..511 of an n_ctx=512 context
+(positions wrap when --steps exceeds 496).  Weights and KV cache are resident
+in HBM before the timed region.
+
+Also reported on the same line:
+  prompt_eval   one 512-token llama_eval (BASELINE.json configs[2]), best of 3
+  roofline      dominant kernel's algorithmic weight bytes per launch / its
+                average duration, HIP events on the launch stream (profiled
+                decode pass right after the timed region)
+  cpu_baseline  the reference AVX2 ggml.c build (oracle/_ref, compiled from
+                /root/reference) on the same file, host cores, bounded sample
+
+Multi-GPU (torchrun): the 7B model does not shard: every rank
+runs an independent replica; value = total tokens of all ranks / max time.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "llama.vk_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+MODEL_BYTES_7B = 4130490880    # algorithmic weight bytes per token
+REF_PUBLISHED_TOKS = 16.3      # 7B Q4_0 predict 61.41 ms/token
+
+
+def prompt_tokens(n):
+    return [1] + [100 + (i * 7919) % 31000 for i in range(1, n)]
+
+
+def dist_setup():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        pg = dist
+    return ws, rank, local, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def all_max(pg, v):
+    if pg is None:
+        return v
+    import torch
+    t = torch.tensor([v], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def ensure_model(path, rank, pg, cfg):
+    if rank == 0 and not os.path.exists(path):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        import lvk
+        tmp = path + ".tmp"
+        lvk.gen_model(tmp, vocab=os.path.join(ROOT, "tests", "golden", "vocab32000.bin"), **cfg)
+        os.replace(tmp, path)
+    barrier(pg)
+
+
+def cpu_baseline(path, budget_s=15.0):
+    """Reference AVX2 ggml.c on the same file (oracle/_ref/libref.so)."""
+    from oracle_lib import REF_SO, Ref
+    if not os.path.exists(REF_SO):
+        return None
+    import numpy as np
+    cores = min(16, len(os.sched_getaffinity(0)))
+    ref = Ref()
+    m = ref.model(path, 512)
+    toks = np.array(prompt_tokens(16), np.int32)
+    t0 = time.time()
+    lg = m.eval(toks, 0, n_threads=cores)
+    t_prompt = time.time() - t0
+    tok, n_past, n_dec, t_dec = int(np.argmax(lg[-1])), 16, 0, 0.0
+    while t_dec < budget_s and n_dec < 256:
+        t0 = time.time()
+        lg = m.eval(np.array([tok], np.int32), n_past, n_threads=cores)
+        t_dec += time.time() - t0
+        tok = int(np.argmax(lg[-1]))
+        n_past += 1
+        n_dec += 1
+    m.close()
+    return {"value": n_dec / t_dec, "unit": "tok/s", "cores": cores, "kind": "reference",
+            "sample": "reference ggml.c AVX2 build (oracle/_ref), same synthetic 7B Q4_0 file, n_ctx 512, f16 KV: "
+                      "16-token prompt (%.2f s) then %d greedy decode steps (%.1f s), %d threads"
+                      % (t_prompt, n_dec, t_dec, cores),
+            "prompt_tok_s": 16 / t_prompt}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=496)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--model", default="/tmp/lvk_bench/llama-7b-q4_0.bin")
+    ap.add_argument("--prompt-evals", type=int, default=3)
+    ap.add_argument("--profile-steps", type=int, default=48)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
+    args = ap.parse_args()
+
+    ws, rank, local, pg = dist_setup()
+    n_gpus = args.gpus if args.gpus else ws
+    import numpy as np
+    import lvk
+    if lvk.device_count() < 1:
+        raise SystemExit("bench: no GPU visible")
+    if ws > 1:
+        lvk.set_device(local % lvk.device_count())
+    cfg = dict(n_embd=4096, n_head=32, n_layer=32, ftype=2, seed=1)
+    ensure_model(args.model, rank, pg, cfg)
+
+    t0 = time.time()
+    m = lvk.Llama(args.model, n_ctx=512)
+    load_s = time.time() - t0
+    n_ctx = 512
+    ptoks = np.array(prompt_tokens(16), np.int32)
+
+    # warmup: prompt + W decode steps (also instantiates the decode graph)
+    lg = m.eval(ptoks, 0)
+    tok, n_past = int(np.argmax(lg[-1])), 16
+    for i in range(args.warmup):
+        lg = m.eval([tok], 16 + (i % (n_ctx - 16)))
+        tok = int(np.argmax(lg[-1]))
+
+    # timed region: K greedy decode steps
+    lg = m.eval(ptoks, 0)
+    tok = int(np.argmax(lg[-1]))
+    barrier(pg)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        lg = m.eval([tok], 16 + (i % (n_ctx - 16)))
+        tok = int(np.argmax(lg[-1]))
+    t1 = time.perf_counter()
+    barrier(pg)
+    elapsed = all_max(pg, t1 - t0)
+    value = n_gpus * args.steps / elapsed
+
+    # prompt eval: one 512-token batch (configs[2])
+    p512 = np.array(prompt_tokens(512), np.int32)
+    best = 1e30
+    for _ in range(args.prompt_evals):
+        t0 = time.perf_counter()
+        m.eval(p512, 0)
+        best = min(best, time.perf_counter() - t0)
+    best = all_max(pg, best)
+    prompt = {"value": n_gpus * 512 / best, "unit": "tok/s", "n_tokens": 512, "ms": best * 1e3,
+              "path": "bit-faithful VALU (v_dot8_i32_i4 + fp32 FMA chains)"}
+
+    # profiled decode pass: HIP events around every kernel class
+    m.set_profiling(True)
+    m.reset_profile()
+    lg = m.eval(ptoks, 0)
+    m.reset_profile()
+    tok = int(np.argmax(lg[-1]))
+    for i in range(args.profile_steps):
+        lg = m.eval([tok], 16 + i * (n_ctx - 17) // max(1, args.profile_steps))
+        tok = int(np.argmax(lg[-1]))
+    prof = m.profile()
+    m.set_profiling(False)
+    kernels = {}
+    for k, v in prof.items():
+        if v["launches"]:
+            avg = v["ms"] / v["launches"]
+            kernels[k] = {"avg_us": avg * 1e3, "ms_per_token": v["ms"] / args.profile_steps,
+                          "gbs": (v["bytes"] / v["launches"]) / (avg * 1e-3) / 1e9 if v["bytes"] else None}
+    dom = max((k for k in kernels if prof[k]["bytes"]), key=lambda k: prof[k]["ms"])
+    bpl = prof[dom]["bytes"] / prof[dom]["launches"]
+    avg_s = prof[dom]["ms"] / prof[dom]["launches"] * 1e-3
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get(dom, {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    achieved = bpl / avg_s / 1e9
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": bpl,
+                "avg_launch_us": avg_s * 1e6}
+    step_gbs = value / n_gpus * MODEL_BYTES_7B / 1e9
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        m.close()
+        cpu = cpu_baseline(args.model, args.cpu_budget)
+
+    if rank == 0:
+        out = {
+            "metric": "decode tok/s + prompt-eval tok/s, LLaMA-7B Q4_0; % HBM roofline",
+            "value": value, "unit": "tok/s", "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": value / REF_PUBLISHED_TOKS,
+            "dtype": "i4xi4->f32 (Q4_0 blocks, exact int dots, fp32 FMA chains)",
+            "data": "synthetic (seeded ggjt 7B Q4_0, lvk-gen-model seed 1)",
+            "config": {"workload": "LLaMA-7B Q4_0 single-stream decode: 16-token prompt then greedy decode over "
+                                   "positions 16..511, n_ctx 512, f16 KV", "n_ctx": n_ctx,
+                       "parallelism": "replicas" if n_gpus > 1 else "single-gpu"},
+            "roofline": roofline,
+            "step_roofline": {"model_bytes_per_token": MODEL_BYTES_7B, "achieved_gbs": step_gbs,
+                              "frac": step_gbs / HBM_PEAK_GBS, "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_7B},
+            "prompt_eval": prompt,
+            "kernels": kernels,
+            "cpu_baseline": cpu,
+            "load_s": load_s,
+        }
+        print(json.dumps(out))
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

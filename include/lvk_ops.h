@@ -22,6 +22,8 @@ extern "C" {
 
 /* number of visible GPUs (0 when none); never fails */
 LVK_API int lvk_device_count(void);
+/* select the HIP device for subsequent contexts/ops of this host thread (hipSetDevice) */
+LVK_API int lvk_set_device(int dev);
 /* version string of the library */
 LVK_API const char * lvk_version(void);
 

@@ -47,6 +47,8 @@ int lvk_device_count(void) {
     return n;
 }
 
+int lvk_set_device(int dev) { return hipSetDevice(dev) == hipSuccess ? 0 : -1; }
+
 const char * lvk_version(void) { return "llama.vk_amd 0.1 (gfx950)"; }
 
 int lvk_quantize_rows(int type, const float * x, int n, int k, void * y) {

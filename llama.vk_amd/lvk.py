@@ -80,6 +80,7 @@ _sig("llama_print_system_info", C.c_char_p, [])
 # lvk_ops.h
 _sig("lvk_device_count", C.c_int, [])
 _sig("lvk_version", C.c_char_p, [])
+_sig("lvk_set_device", C.c_int, [C.c_int])
 _sig("lvk_quantize_rows", C.c_int, [C.c_int, f32p, C.c_int, C.c_int, u8p])
 _sig("lvk_mul_mat_q", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, f32p, C.c_int, f32p])
 _sig("lvk_mul_mat_q_norm", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, f32p, f32p, C.c_int, f32p])
@@ -248,6 +249,10 @@ def host_tables():
     s = np.zeros(65536, np.uint16)
     lib.lvk_host_tables(e, s)
     return e, s
+
+
+def set_device(dev):
+    _check(lib.lvk_set_device(dev), "lvk_set_device")
 
 
 def device_count():
