@@ -47,123 +47,142 @@ __device__ __forceinline__ float quad_f16dot_reduce(const float s[8]) {
 }
 
 // ---------------------------------------------------------------------------
-// scores[t][h][p] = (K[p,h,:] . f16(q[t,h,:])) * scale, or -inf when masked.
-// grid (ceil(n_ctx/64), H, N), 256 threads: quad = one position.
+// Fused attention for one (token t, head h, half of the head dims):
+//   phase 1  scores of every position p < n_kv into LDS (quad = one position,
+//            4 passes of 64 positions in flight per unrolled step)
+//   phase 2  softmax in LDS, P rounded to f16
+//   phase 3  P.V for HD/2 output dims (quad = one dim), V loads unrolled x8
+//   phase 4  quantize the HD/2 outputs (HD/64 weight blocks) for Wo
+// grid (H, N, 2), 256 threads.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_attn_scores(const uint16_t * __restrict__ q16, const uint16_t * __restrict__ kc,
-                                                     float * __restrict__ scores, const StepParams * sp,
-                                                     int E, int hd, int n_ctx, float scale) {
+template <int HD, int QT>
+__global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16, const uint16_t * __restrict__ kc,
+                                              const uint16_t * __restrict__ vc, const uint16_t * __restrict__ exp_tab,
+                                              ActQ out, const StepParams * sp, int E, int n_ctx, float scale,
+                                              float * __restrict__ scores_dbg, float * __restrict__ out_f32,
+                                              uint16_t * __restrict__ p16_out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NSTEP = HD / 32;
     const int n_past = sp->n_past, N = sp->n_tokens;
     const int n_kv = n_past + N;
-    const int t = blockIdx.z, h = blockIdx.y;
-    const int p = blockIdx.x * 64 + (threadIdx.x >> 2);
-    const int r = threadIdx.x & 3;
-    if (blockIdx.x * 64 >= n_kv || t >= N) return;
-    const bool valid = p < n_kv;
-    const bool masked = p > n_past + t;
-    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (valid && !masked) {
-        const uint4 * kp = (const uint4 *) (kc + (size_t) p * E + h * hd) + r;
-        const uint4 * qp = (const uint4 *) (q16 + (size_t) t * E + h * hd) + r;
-        for (int step = 0; step < hd / 32; ++step) {
-            float kf[8], qf[8];
-            unpack8h(kp[step * 4], kf);
-            unpack8h(qp[step * 4], qf);
+    const int h = blockIdx.x, t = blockIdx.y, half = blockIdx.z;
+    if (t >= N) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = tid & 3;
+    float * sc = (float *) smem;                                   // n_ctx scores / exp values
+    uint16_t * p16 = (uint16_t *) (smem + (size_t) n_ctx * 4);     // n_ctx f16 probabilities
+    float * red = (float *) (smem + (size_t) n_ctx * 6);           // 8 floats
+    double * redd = (double *) (smem + (size_t) n_ctx * 6 + 32);   // 4 doubles
+    const int lim = n_past + t;                                    // last unmasked position
+
+    // ---- phase 1: KQ (ggml_vec_dot_f16 over HD, Q in f16) ----
+    uint4 qv[NSTEP];
+    {
+        const uint4 * qp = (const uint4 *) (q16 + (size_t) t * E + h * HD) + r;
 #pragma unroll
-            for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(kf[l], qf[l], s[l]);
+        for (int st = 0; st < NSTEP; ++st) qv[st] = qp[st * 4];
+    }
+    const int npos = min(n_kv, lim + 1);     // masked positions get -inf without a dot
+    for (int p0 = 0; p0 < npos; p0 += 128) {
+        uint4 kv0[NSTEP], kv1[NSTEP];
+        const int pa = min(p0 + (tid >> 2), npos - 1), pb = min(p0 + 64 + (tid >> 2), npos - 1);
+        const uint4 * ka = (const uint4 *) (kc + (size_t) pa * E + h * HD) + r;
+        const uint4 * kb = (const uint4 *) (kc + (size_t) pb * E + h * HD) + r;
+#pragma unroll
+        for (int st = 0; st < NSTEP; ++st) { kv0[st] = ka[st * 4]; kv1[st] = kb[st * 4]; }
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int st = 0; st < NSTEP; ++st) {
+                float kf[8], qf[8];
+                unpack8h(hh ? kv1[st] : kv0[st], kf);
+                unpack8h(qv[st], qf);
+#pragma unroll
+                for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(kf[l], qf[l], s[l]);
+            }
+            const float kq = quad_f16dot_reduce(s);
+            const int p = p0 + hh * 64 + (tid >> 2);
+            if (r == 0 && p < npos) sc[p] = kq * scale;      // ggml_vec_scale_f32 (llama.cpp:1026)
         }
     }
-    const float kq = quad_f16dot_reduce(s);
-    if (valid && r == 0) {
-        const float v = kq * scale;                   // ggml_vec_scale_f32
-        scores[((size_t) t * gridDim.y + h) * n_ctx + p] = masked ? -INFINITY : v;
-    }
-}
+    for (int p = npos + tid; p < n_kv; p += 256) sc[p] = -INFINITY;   // ggml.c:7028-7031
+    __syncthreads();
+    if (scores_dbg && half == 0)
+        for (int p = tid; p < n_kv; p += 256) scores_dbg[((size_t) t * gridDim.x + h) * n_ctx + p] = sc[p];
 
-// ---------------------------------------------------------------------------
-// softmax + P.V for 32 output dims of one head and one token, then quantize
-// those 32 values (one weight block) for the Wo matvec.
-// grid (hd/32, H, N), 128 threads: quad = one output dim.
-// ---------------------------------------------------------------------------
-template <int QT>
-__global__ __launch_bounds__(128) void k_attn_pv(const float * __restrict__ scores, const uint16_t * __restrict__ vc,
-                                                 const uint16_t * __restrict__ exp_tab, ActQ out,
-                                                 const StepParams * sp, int E, int hd, int n_ctx,
-                                                 float * __restrict__ out_f32, uint16_t * __restrict__ p16_out) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int n_past = sp->n_past, N = sp->n_tokens;
-    const int n_kv = n_past + N;
-    const int t = blockIdx.z, h = blockIdx.y, dc = blockIdx.x;
-    if (t >= N) return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    float * ev = (float *) smem;                                        // n_ctx floats
-    uint16_t * p16 = (uint16_t *) (smem + (size_t) n_ctx * 4);          // n_ctx halves (+32 pad)
-    float * red = (float *) (smem + (size_t) n_ctx * 6 + 64);           // small scratch
-    double * redd = (double *) (red + 16);
-    const float * srow = scores + ((size_t) t * gridDim.y + h) * n_ctx;
-
-    // softmax (ggml.c:7099-7121)
+    // ---- phase 2: softmax (ggml.c:7099-7121) ----
     float mx = -INFINITY;
-    for (int p = tid; p < n_kv; p += 128) { const float v = srow[p]; mx = v > mx ? v : mx; }
+    for (int p = tid; p < n_kv; p += 256) { const float v = sc[p]; mx = v > mx ? v : mx; }
     mx = warp_max(mx);
     if (lane == 0) red[wave] = mx;
     __syncthreads();
-    mx = red[0] > red[1] ? red[0] : red[1];
+    {
+        const float a = red[0] > red[1] ? red[0] : red[1], b = red[2] > red[3] ? red[2] : red[3];
+        mx = a > b ? a : b;
+    }
     double sum = 0.0;   // exact in any order: every term is an fp16 value in [0,1]
-    for (int p = tid; p < n_kv; p += 128) {
-        const float v = srow[p];
+    for (int p = tid; p < n_kv; p += 256) {
+        const float v = sc[p];
         float e = 0.0f;
         if (v != -INFINITY) {
             e = f16_to_f32(exp_tab[f32_to_f16(v - mx)]);
             sum += (double) e;
         }
-        ev[p] = e;
+        sc[p] = e;
     }
     sum = warp_sum_d(sum);
     if (lane == 0) redd[wave] = sum;
     __syncthreads();
-    sum = redd[0] + redd[1];
-    const float sc = (float) (1.0 / sum);
+    sum = (redd[0] + redd[1]) + (redd[2] + redd[3]);
+    const float scl = (float) (1.0 / sum);
     const int n_pad = (n_kv + 31) & ~31;
-    for (int p = tid; p < n_pad; p += 128) p16[p] = p < n_kv ? f32_to_f16(ev[p] * sc) : (uint16_t) 0;
+    for (int p = tid; p < n_pad; p += 256) p16[p] = p < n_kv ? f32_to_f16(sc[p] * scl) : (uint16_t) 0;
     __syncthreads();
-    if (p16_out && dc == 0)
-        for (int p = tid; p < n_kv; p += 128) p16_out[((size_t) t * gridDim.y + h) * n_ctx + p] = p16[p];
+    if (p16_out && half == 0)
+        for (int p = tid; p < n_kv; p += 256) p16_out[((size_t) t * gridDim.x + h) * n_ctx + p] = p16[p];
 
-    // KQV: ggml_vec_dot_f16(n_kv, V row, P)
-    const int d = dc * 32 + (tid >> 2);
-    const int r = tid & 3;
-    const uint16_t * vrow = vc + (size_t) (h * hd + d) * n_ctx;
+    // ---- phase 3: KQV = ggml_vec_dot_f16(n_kv, V row, P) ----
+    const int d = half * (HD / 2) + (tid >> 2);
+    const uint16_t * vrow = vc + (size_t) (h * HD + d) * n_ctx;
     const int np = n_kv & ~31;
-    const int lim = n_past + t;       // last unmasked position of this column
+    const int nsteps = min(np, lim + 1 + 31) / 32;     // steps holding at least one unmasked position
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < np && i <= lim; i += 32) {      // fully masked steps add exact zeros: skipped
-        float vf[8], pf[8];
-        unpack8h(*((const uint4 *) (vrow + i) + r), vf);
-        unpack8h(*((const uint4 *) (p16 + i) + r), pf);
+    for (int i0 = 0; i0 < nsteps; i0 += 8) {
+        uint4 vv[8];
 #pragma unroll
-        for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(vf[l], pf[l], s[l]);
+        for (int u = 0; u < 8; ++u) vv[u] = *((const uint4 *) (vrow + min(i0 + u, nsteps - 1) * 32) + r);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (i0 + u < nsteps) {
+                float vf[8], pf[8];
+                unpack8h(vv[u], vf);
+                unpack8h(*((const uint4 *) (p16 + (i0 + u) * 32) + r), pf);
+#pragma unroll
+                for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(vf[l], pf[l], s[l]);
+            }
+        }
     }
     const float res = quad_f16dot_reduce(s);
     float o = res;
     if (r == 0) {
-        double sumf = (double) res;
+        double sumf = (double) res;               // leftovers in double (ggml.c:1806-1808)
         for (int i = np; i < n_kv && i <= lim; ++i) {
             const float pr = f16_to_f32(vrow[i]) * f16_to_f32(p16[i]);
             sumf += (double) pr;
         }
         o = (float) sumf;
     }
-    // gather the 32 outputs in LDS, quantize as one block (quantize_row_q4_x)
+    if (r == 0 && out_f32) out_f32[(size_t) t * E + h * HD + d] = o;
+
+    // ---- phase 4: quantize HD/2 outputs = HD/64 weight blocks ----
     __syncthreads();
-    float * ob = ev;
+    float * ob = sc;
     if (r == 0) ob[tid >> 2] = o;
-    if (r == 0 && out_f32) out_f32[(size_t) t * E + h * hd + d] = o;
     __syncthreads();
-    if (wave == 0 && lane < 32) {
-        const float v = ob[lane];
-        const int blk = (h * hd + dc * 32) / 32;
-        uint32_t * scratch = (uint32_t *) (ev + 64);
+    if (tid < HD / 2) {
+        const float v = ob[tid];
+        const int blk = (h * HD + half * (HD / 2)) / 32 + (tid >> 5);
+        uint32_t * scratch = (uint32_t *) (sc + 128) + (tid >> 5) * 4;
         if constexpr (QT == Q4_0) {
             float amax = fabsf(v);
             for (int o2 = 16; o2 > 0; o2 >>= 1) { const float w = __shfl_xor(amax, o2); amax = w > amax ? w : amax; }
@@ -174,9 +193,9 @@ __global__ __launch_bounds__(128) void k_attn_pv(const float * __restrict__ scor
             part |= __shfl_xor(part, 1);
             part |= __shfl_xor(part, 2);
             part |= __shfl_xor(part, 4);
-            if ((lane & 7) == 0) scratch[lane >> 3] = part;
+            if ((lane & 7) == 0) scratch[(lane & 31) >> 3] = part;
             __builtin_amdgcn_wave_barrier();
-            if (lane == 0) {
+            if ((lane & 31) == 0) {
                 out.d[(size_t) t * out.nb + blk] = dd;
                 out.qs[(size_t) t * out.nb + blk] = make_uint4(scratch[0], scratch[1], scratch[2], scratch[3]);
             }
@@ -188,15 +207,13 @@ __global__ __launch_bounds__(128) void k_attn_pv(const float * __restrict__ scor
 
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s) {
     const int hd = A.n_embd / A.n_head;
-    if (hd % 32 || A.n_ctx % 32) return hipErrorInvalidValue;
+    if (hd != 128 || A.n_ctx % 32 || A.n_ctx < 128) return hipErrorInvalidValue;
     if (A.out_qtype != Q4_0) return hipErrorNotSupported;
     const float scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
-    dim3 g1((A.n_ctx + 63) / 64, A.n_head, A.n_tokens);
-    hipLaunchKernelGGL(k_attn_scores, g1, dim3(256), 0, s, A.q16, A.kc, A.scores, A.sp, A.n_embd, hd, A.n_ctx, scale);
-    dim3 g2(hd / 32, A.n_head, A.n_tokens);
-    const size_t lds = (size_t) A.n_ctx * 6 + 64 + 256;
-    hipLaunchKernelGGL(k_attn_pv<Q4_0>, g2, dim3(128), lds, s, A.scores, A.vc, A.exp_tab, A.out, A.sp,
-                       A.n_embd, hd, A.n_ctx, A.out_f32, A.p16_out);
+    dim3 grid(A.n_head, A.n_tokens, 2);
+    const size_t lds = (size_t) A.n_ctx * 6 + 64;
+    hipLaunchKernelGGL((k_attn<128, Q4_0>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,
+                       A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out);
     return hipGetLastError();
 }
 

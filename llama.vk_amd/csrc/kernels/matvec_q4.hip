@@ -326,38 +326,37 @@ __global__ __launch_bounds__(NT) void k_matvec_q40(Params P) {
         const int nunits = P.K / 8;
 #pragma unroll
         for (int k = 0; k < UMAX; ++k) {
-            const int u = k * NT + tid;
-            if (u < nunits) {
-                const float4 * gp = (const float4 *) (P.g + (size_t) u * 8);
-                const float4 * xp = (const float4 *) (P.x + (size_t) (P.tok0 + t0) * P.K + (size_t) u * 8);
-                gv[k][0] = gp[0]; gv[k][1] = gp[1];
-                xv[k][0] = xp[0]; xv[k][1] = xp[1];
-            }
+            // unconditional (clamped) loads keep the vmcnt bookkeeping static
+            const int u = min(k * NT + tid, nunits - 1);
+            const float4 * gp = (const float4 *) (P.g + (size_t) u * 8);
+            const float4 * xp = (const float4 *) (P.x + (size_t) (P.tok0 + t0) * P.K + (size_t) u * 8);
+            gv[k][0] = gp[0]; gv[k][1] = gp[1];
+            xv[k][0] = xp[0]; xv[k][1] = xp[1];
         }
     }
     if constexpr (PRE && PRO == PRO_ACTQ) {
 #pragma unroll
         for (int k = 0; k < BMAX; ++k) {
-            const int b = k * NT + tid;
-            if (b < nb) {
-                qv[k] = P.xq.qs[(size_t) (P.tok0 + t0) * nb + b];
-                dv[k] = P.xq.d[(size_t) (P.tok0 + t0) * nb + b];
-            }
+            const int b = min(k * NT + tid, nb - 1);
+            qv[k] = P.xq.qs[(size_t) (P.tok0 + t0) * nb + b];
+            dv[k] = P.xq.d[(size_t) (P.tok0 + t0) * nb + b];
         }
     }
 
-    // 2. weight stream: D chunks in flight
+    // 2. weight stream: D chunks in flight.  Every iteration issues its loads
+    //    unconditionally (past-the-end chunks re-read the last one, an L1/L2
+    //    hit), so the compiler's in-order vmcnt bookkeeping stays exact and
+    //    waits only for the chunk being consumed (3*(D-1) loads left in flight).
     const uint4 * nib = P.nib + (size_t) g * C * 2 * 64 + lane;
     const float2 * scl = P.scl + (size_t) g * C * 64 + lane;
     uint4 W0[D], W1[D];
     float2 S[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-        if (d < C) {
-            W0[d] = ld_nt(nib + (size_t) d * 128);
-            W1[d] = ld_nt(nib + (size_t) d * 128 + 64);
-            S[d] = scl[(size_t) d * 64];
-        }
+        const int cl = min(d, C - 1);
+        W0[d] = ld_nt(nib + (size_t) cl * 128);
+        W1[d] = ld_nt(nib + (size_t) cl * 128 + 64);
+        S[d] = scl[(size_t) cl * 64];
     }
 
     // 3. activation table
@@ -373,19 +372,16 @@ __global__ __launch_bounds__(NT) void k_matvec_q40(Params P) {
 #pragma unroll
     for (int tt = 0; tt < T; ++tt) acc[tt][0] = acc[tt][1] = 0.0f;
 
-    for (int c0 = 0; c0 < C; c0 += D) {
+    const int ngrp = (C + D - 1) / D;
+    for (int gi = 0; gi < ngrp; ++gi) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            const int c = c0 + d;
-            if (c < C) {
-                chunk_q40<T>(acc, W0[d], W1[d], S[d], tbl_base, dx_base, c, q, nb);
-                const int cn = c + D;
-                if (cn < C) {
-                    W0[d] = ld_nt(nib + (size_t) cn * 128);
-                    W1[d] = ld_nt(nib + (size_t) cn * 128 + 64);
-                    S[d] = scl[(size_t) cn * 64];
-                }
-            }
+            const int c = gi * D + d;
+            if (c < C) chunk_q40<T>(acc, W0[d], W1[d], S[d], tbl_base, dx_base, c, q, nb);
+            const int cn = min(c + D, C - 1);
+            W0[d] = ld_nt(nib + (size_t) cn * 128);
+            W1[d] = ld_nt(nib + (size_t) cn * 128 + 64);
+            S[d] = scl[(size_t) cn * 64];
         }
     }
 
@@ -489,7 +485,7 @@ hipError_t launch_matvec(const MvLaunch & L, int pro, int epi, hipStream_t s) {
             if (pro != PRO_NORM || ng % 2) return hipErrorInvalidValue;
             if (P.K > 8192) return hipErrorInvalidValue;
             return prefill ? go<128, 4, 8, PRO_NORM, EPI_QKV, 4>(P, ng, N, s)
-                           : go<128, 1, 8, PRO_NORM, EPI_QKV, 8>(P, ng, N, s);
+                           : go<128, 1, 8, PRO_NORM, EPI_QKV, 12>(P, ng, N, s);
         case EPI_SWIGLU:
             if (pro != PRO_NORM || ng % 4 || P.K > 8192) return hipErrorInvalidValue;
             return prefill ? go<256, 4, 4, PRO_NORM, EPI_SWIGLU, 4>(P, ng, N, s)
@@ -502,12 +498,12 @@ hipError_t launch_matvec(const MvLaunch & L, int pro, int epi, hipStream_t s) {
             }
             if (P.nb > 12 * 64) return hipErrorInvalidValue;
             return prefill ? go<64, 4, 12, PRO_ACTQ, EPI_STORE, 4>(P, ng, N, s)
-                           : go<64, 1, 12, PRO_ACTQ, EPI_STORE, 8>(P, ng, N, s);
+                           : go<64, 1, 12, PRO_ACTQ, EPI_STORE, 16>(P, ng, N, s);
         case EPI_RESID:
             if (pro != PRO_ACTQ) return hipErrorInvalidValue;
             if (P.nb > 12 * 64) return hipErrorInvalidValue;
             return prefill ? go<64, 4, 12, PRO_ACTQ, EPI_RESID, 4>(P, ng, N, s)
-                           : go<64, 1, 12, PRO_ACTQ, EPI_RESID, 8>(P, ng, N, s);
+                           : go<64, 1, 12, PRO_ACTQ, EPI_RESID, 16>(P, ng, N, s);
     }
     return hipErrorInvalidValue;
 }
