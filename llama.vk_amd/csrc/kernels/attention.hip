@@ -212,7 +212,7 @@ hipError_t launch_attention(const AttnLaunch & A, hipStream_t s) {
     const float scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
     dim3 grid(A.n_head, A.n_tokens, 2);
     const size_t lds = (size_t) A.n_ctx * 6 + 64;
-    hipLaunchKernelGGL((k_attn<128, Q4_0>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,
+    LVK_LAUNCH((k_attn<128, Q4_0>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,
                        A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out);
     return hipGetLastError();
 }

@@ -42,9 +42,12 @@ __device__ __forceinline__ float quad_get(float v, int k) {
     }
 }
 
-// signed int4 x int4 8-way dot (v_dot8_i32_i4)
+// signed int4 x int4 8-way dot (v_dot8_i32_i4, VOP3P with an inline 0
+// accumulator: the builtin lowers to v_dot8c + a v_mov of the 0 per call)
 __device__ __forceinline__ int dot8(uint32_t a, uint32_t b) {
-    return __builtin_amdgcn_sdot8((int) a, (int) b, 0, false);
+    int r;
+    asm("v_dot8_i32_i4 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 // unsigned u4 x u4 8-way dot (v_dot8_u32_u4)
 __device__ __forceinline__ int udot8(uint32_t a, uint32_t b) {
@@ -62,6 +65,33 @@ __device__ __forceinline__ uint4 ld_nt(const uint4 * p) {
 __device__ __forceinline__ double warp_sum_d(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
+}
+// whole-wave double sum through DPP (quad xor 1, xor 2, half-row and row
+// mirrors) and four readlanes; every lane returns the same value, and the
+// association order is fixed: ((row0 + row1) + (row2 + row3)) of 16-lane trees
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int2 i = __builtin_bit_cast(int2, v);
+    int2 o;
+    o.x = __builtin_amdgcn_mov_dpp(i.x, CTRL, 0xF, 0xF, false);
+    o.y = __builtin_amdgcn_mov_dpp(i.y, CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, o);
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+    v += dpp_d<0xB1>(v);     // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v);     // quad_perm [2,3,0,1]
+    v += dpp_d<0x141>(v);    // row_half_mirror
+    v += dpp_d<0x140>(v);    // row_mirror
+    const int2 i = __builtin_bit_cast(int2, v);
+    double r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int2 o;
+        o.x = __builtin_amdgcn_readlane(i.x, 16 * k);
+        o.y = __builtin_amdgcn_readlane(i.y, 16 * k);
+        r[k] = __builtin_bit_cast(double, o);
+    }
+    return (r[0] + r[1]) + (r[2] + r[3]);
 }
 __device__ __forceinline__ float warp_max(float v) {
     for (int o = 32; o > 0; o >>= 1) { const float w = __shfl_xor(v, o); v = w > v ? w : v; }

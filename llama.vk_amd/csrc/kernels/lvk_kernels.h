@@ -4,22 +4,41 @@
 // so the decode step can be recorded into one hipGraph.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace lvk {
+
+// Profiling hook: when a launcher runs with these set (one kernel per timed
+// launch), the kernel is dispatched with hipExtLaunchKernelGGL and the two
+// events are stamped by the command processor at its start and end -- the
+// same interval rocprofv3's kernel trace reports.
+struct LaunchEvents {
+    hipEvent_t start = nullptr;
+    hipEvent_t stop = nullptr;
+};
+extern thread_local LaunchEvents g_launch_events;
+
+#define LVK_LAUNCH(kern, grid, block, lds, stream, ...)                                                        \
+    do {                                                                                                       \
+        if (::lvk::g_launch_events.start)                                                                      \
+            hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ::lvk::g_launch_events.start,                \
+                                  ::lvk::g_launch_events.stop, 0, __VA_ARGS__);                                \
+        else                                                                                                   \
+            hipLaunchKernelGGL(kern, grid, block, lds, stream, __VA_ARGS__);                                   \
+    } while (0)
 
 enum QType : int { Q4_0 = 2, Q4_1 = 3 };
 
 // ---------------------------------------------------------------------------
 // Device weight image of one quantized matrix W[M][K] (ggml row-major, K = row
-// length) in the "quad-sliced" layout:
-//   rows are grouped 16 per wavefront; lane l = 4*r + q of the wave owns row r
-//   of the group and the two AVX2 accumulator chains j = 2q, 2q+1 of the
-//   reference dot product (ggml.c:1950-2026).
-//   nib : [M/16][K/256][2][64] uint4   -- nibble slices, 8 blocks per chunk
-//   scl : [M/16][K/256][64]   float2  -- Q4_0: d of blocks 8c+q, 8c+4+q
-//                                        (Q4_1: float4 {d0,d1,m0,m1})
-// Bytes per row equal the file's (20 B / 24 B per 32 weights).
+// length) in the "octet" layout: rows are grouped 8 per
+// wavefront; lane l = 8*r + j owns row r of the group and the AVX2 accumulator
+// chain j of the reference dot product (ggml.c:1950-2026).  NC = ceil(K/1024).
+//   nib : [M/8][NC][4][64] uint4   -- nibble slices of 8 blocks per uint4
+//   scl : [M/8][NC][64]   float4  -- d of blocks 32c+8m+j, m = 0..3
+// Bytes per row equal the file's (20 B per 32 weights; the last chunk of a
+// row is zero-padded to 32 blocks when K % 1024 != 0 and never streamed).
 struct QMatrix {
     int qtype = Q4_0;
     int M = 0, K = 0;
@@ -49,9 +68,9 @@ struct RopeTable {            // host-built with glibc powf/cosf/sinf (ggml.c:72
 };
 
 // prologue (how the matvec obtains its quantized input)
-enum Pro : int { PRO_NORM = 0, PRO_ACTQ = 1 };
+enum Pro : int { PRO_NORM = 0, PRO_ACTQ = 1, PRO_ACTF = 2 /* f32 input, quantize only */ };
 // epilogue (what it does with row results)
-enum Epi : int { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_SWIGLU = 3 };
+enum Epi : int { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_SWIGLU_F32 = 4 };
 
 struct MvLaunch {
     QMatrix w;
@@ -74,9 +93,16 @@ struct MvLaunch {
     // EPI_SWIGLU
     const uint16_t * silu_tab = nullptr;   // 64Ki fp16 table
     ActQ out_q;                            // quantized u = silu(w1 x) * (w3 x)
+    float * u = nullptr;                   // EPI_SWIGLU_F32: u in f32 [N][M/2]
 };
 
 hipError_t launch_matvec(const MvLaunch & L, int pro, int epi, hipStream_t s);
+
+// single-token decode matvec, one workgroup per CU (matvec_cu.hip).  Row
+// lengths compiled in: matvec_cu_supported(K).  Returns hipErrorNotSupported
+// for anything else (the caller then uses launch_matvec).
+bool matvec_cu_supported(int K);
+hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s);
 
 // token embedding rows: x[t] = dequant(tok_emb[tokens[t]]) (ggml.c:6868-6895)
 hipError_t launch_embed(const void * emb, int emb_type, int n_embd, const int * tokens, int n,
@@ -99,8 +125,13 @@ struct AttnLaunch {
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
 
 // one-time weight repack: file-layout rows (ggml blocks) -> quad-sliced image
+// interleave4: src_rows holds two (M/2)-row matrices A then B; the image
+// interleaves them per 4 rows (A0-3, B0-3, A4-7, ...: the fused W1|W3)
 hipError_t launch_repack(const void * src_rows, int qtype, int M, int K, uint4 * nib, void * scl,
-                         hipStream_t s);
+                         hipStream_t s, int interleave4 = 0);
+// bytes of the two image arrays for an M x K matrix
+inline size_t qimage_nib_bytes(int M, int K) { return (size_t) M * ((K / 32 + 31) / 32) * 512; }
+inline size_t qimage_scl_bytes(int M, int K) { return (size_t) M * ((K / 32 + 31) / 32) * 128; }
 
 // operator-level helpers used by the C ABI tests
 hipError_t launch_quantize_act(const float * x, int N, int K, int qtype, ActQ out, hipStream_t s);

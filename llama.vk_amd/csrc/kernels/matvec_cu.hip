@@ -1,0 +1,485 @@
+// matvec_cu.hip -- CU-balanced single-token Q4_0 matvec (the decode hot path).
+//
+// Same arithmetic as matvec_q4.hip (bit-faithful ggml_vec_dot_q4_0 AVX2
+// chains, ggml.c:1950-2026, on an activation quantized by quantize_row_q4_0,
+// ggml.c:621-685), organised for the batch-1 weight stream:
+//
+//   * A decode matvec reads every weight byte once, so it is bound by how fast
+//     each CU can pull bytes (~25-30 GB/s per CU; MI355X_MICROARCH.md, HBM) and
+//     by how evenly the bytes are spread over the 256 CUs.  The grid is one
+//     workgroup per CU and workgroup w owns row groups [w*G/n, (w+1)*G/n)
+//     (a row group = 8 rows = one wavefront's work), so every CU streams the
+//     same number of bytes (+-1 row group).
+//   * The activation table (RMSNorm + quantize, or a plain quantize) is built
+//     once per workgroup in LDS while the first D chunks of weights are
+//     already in flight.
+//   * Each wave walks its row groups with a D-chunk register prefetch that
+//     runs across group boundaries, so a CU's weight stream never drains
+//     between groups.  Row length K is a template constant: all loads are
+//     exact and static (hipcc's vmcnt accounting stays precise).
+#include "lvk_device.h"
+#include "lvk_kernels.h"
+#include "matvec_common.h"
+
+namespace lvk {
+
+namespace {
+using namespace mv;
+
+#ifdef LVK_PROBE_TIMING   // dev probe builds only: per-wave s_memtime trace
+__device__ unsigned long long g_trace[256 * 16 * 64];
+#define LVK_T(ev)                                                                                  \
+    do {                                                                                           \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
+        if (lane == 0 && (ev) < 64) g_trace[((blockIdx.x & 255) * 16 + (wave & 15)) * 64 + (ev)] = t_; \
+    } while (0)
+#else
+#define LVK_T(ev) do { } while (0)
+#endif
+
+struct CuParams {
+    const uint4 * nib;
+    const float4 * scl;
+    int G;                      // row groups (M / 8)
+    const float * x;            // PRO_NORM / PRO_ACTF: f32 input [K]
+    const float * g;            // PRO_NORM: norm weight [K]
+    ActQ xq;                    // PRO_ACTQ: quantized input
+    const StepParams * sp;
+    float * y;                  // EPI_STORE / EPI_RESID
+    float * u;                  // EPI_SWIGLU_F32: silu(w1 x) * (w3 x) [M/2]
+    uint16_t * q16;
+    uint16_t * kc;
+    uint16_t * vc;
+    const float2 * rope;
+    int n_embd, head_dim, n_ctx;
+    const uint16_t * silu_tab;
+};
+
+template <int NW, int NP, int D, int PRO, int EPI, int KT>
+__global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
+    constexpr int PT = NP * 64;                 // prologue threads
+    constexpr int nb = KT / 32;                 // blocks per row
+    constexpr int nsub = nb / 8;                // 8-block sub-chunks (one uint4 per lane each)
+    constexpr int NC = (nb + 31) / 32;          // chunks of 32 blocks
+    constexpr bool XG = (NC % D) == 0;          // prefetch may cross into the next group
+    constexpr int nunits = KT / 8;              // f32 prologue work units (8 elements)
+    static_assert(D <= NC, "prefetch deeper than a row");
+    static_assert(nb % 8 == 0, "K must be a multiple of 256");
+
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t * act = (uint32_t *) smem;                          // nb * 32 B
+    float * dxp = (float *) (smem + nb * 32);                    // NC * 128 B
+    float * sbuf = dxp + NC * 32;                                // NW * 2 * 256 floats
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
+    int tq = 4;   // trace event index (probe builds)
+    LVK_T(0);
+
+    if (NP > 0 && wave >= NW) {
+        // ---- prologue waves: build the activation table while the compute
+        // waves put the CU's weight stream in flight (they never wait on x)
+        const int pt = tid - NW * 64;
+        constexpr int PT_ = PT > 0 ? PT : 64;   // (NP == 0: branch never taken)
+        if constexpr (PRO == PRO_NORM || PRO == PRO_ACTF) {
+            constexpr int UMP = (nunits + PT_ - 1) / PT_;
+            float4 xv[UMP][2];
+            float4 gv[PRO == PRO_NORM ? UMP : 1][2];
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                const int un = min(k * PT_ + pt, nunits - 1);
+                const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
+                xv[k][0] = xp[0]; xv[k][1] = xp[1];
+                if constexpr (PRO == PRO_NORM) {
+                    const float4 * gp = (const float4 *) (P.g + (size_t) un * 8);
+                    gv[k][0] = gp[0]; gv[k][1] = gp[1];
+                }
+            }
+            float scale = 1.0f;
+            if constexpr (PRO == PRO_NORM) {
+                // ggml_compute_forward_rms_norm_f32 (ggml.c:6058-6076): every
+                // prologue wave sums all K squares itself (lane-strided, then a
+                // butterfly that leaves the same double in every lane), so no
+                // cross-wave reduction is needed.  Terms are float squares
+                // carried in double (RMSNorm order).
+                constexpr int XPL = KT / 4 / 64;
+                float4 xs[XPL];
+#pragma unroll
+                for (int i = 0; i < XPL; ++i) xs[i] = ((const float4 *) P.x)[i * 64 + lane];
+                double acc = 0.0;
+#pragma unroll
+                for (int i = 0; i < XPL; ++i) {
+                    const float e[4] = {xs[i].x, xs[i].y, xs[i].z, xs[i].w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) { const float sq = e[q] * e[q]; acc += (double) sq; }
+                }
+                LVK_T(56);
+                acc = warp_sum_d(acc);
+                const float mean = (float) (acc / (double) KT);
+                scale = 1.0f / sqrtf(mean + 1e-6f);
+                LVK_T(57);
+            }
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                if (k * PT_ >= nunits) break;
+                const int un = k * PT_ + pt;
+                float v[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
+                              xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
+                float amax = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if constexpr (PRO == PRO_NORM) {
+                        const float gg[8] = {gv[k][0].x, gv[k][0].y, gv[k][0].z, gv[k][0].w,
+                                             gv[k][1].x, gv[k][1].y, gv[k][1].z, gv[k][1].w};
+                        const float yn = v[e] * scale;      // ggml_vec_scale_f32 (ggml.c:6076)
+                        v[e] = gg[e] * yn;                  // ggml_mul(repeat(g), cur) (llama.cpp:984)
+                    }
+                    const float a = fabsf(v[e]);
+                    amax = a > amax ? a : amax;
+                }
+                // the 4 units of a block are a lane quad: block amax (ggml.c:636-649)
+                const float o0 = quad_bcast<0>(amax), o1 = quad_bcast<1>(amax);
+                const float o2 = quad_bcast<2>(amax), o3 = quad_bcast<3>(amax);
+                const float m01 = o1 > o0 ? o1 : o0, m23 = o3 > o2 ? o3 : o2;
+                amax = m23 > m01 ? m23 : m01;
+                const float d = amax / 7.0f;                              // ggml.c:651
+                const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;     // ggml.c:653
+                const uint32_t w = q40_pack8(v, id);
+                if (un < nunits) act_store(act, dxp, un >> 2, un & 3, w, d, (un & 3) == 0);
+            }
+        } else {
+            constexpr int UMP = (nb + PT_ - 1) / PT_;
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                const int b = k * PT_ + pt;
+                if (b < nb) {
+                    const uint4 qs = P.xq.qs[b];
+                    const float d = P.xq.d[b];
+                    act_store(act, dxp, b, 0, qs.x, d, true);
+                    act_store(act, dxp, b, 1, qs.y, 0.0f, false);
+                    act_store(act, dxp, b, 2, qs.z, 0.0f, false);
+                    act_store(act, dxp, b, 3, qs.w, 0.0f, false);
+                }
+            }
+        }
+        LVK_T(2);
+        __syncthreads();
+        return;
+    }
+
+    // ---- compute waves
+    const int j = lane & 7;
+    const int r = lane >> 3;
+    const int nwg = gridDim.x;
+    const int g0 = (int) (blockIdx.x * (unsigned) P.G / (unsigned) nwg);     // G * n_cu < 2^32
+    const int g1 = (int) ((blockIdx.x + 1) * (unsigned) P.G / (unsigned) nwg);
+    const int ng = max(0, (g1 - g0 - wave + NW - 1) / NW);      // row groups of this wave
+    if (NP > 0 && ng == 0) { __syncthreads(); return; }
+    int gc = min(g0 + wave, P.G - 1);
+
+    // NP == 0: the compute waves build the activation table themselves; its
+    // inputs are issued first (vmcnt retires in order)
+    constexpr int NT = NW * 64;
+    constexpr bool FPRO = (PRO == PRO_NORM || PRO == PRO_ACTF);
+    constexpr int UM = NP > 0 ? 1 : (FPRO ? (nunits + NT - 1) / NT : (nb + NT - 1) / NT);
+    float4 xv[UM][2];
+    float4 gv[UM][2];
+    uint4 qv[UM];
+    float dv[UM];
+    if constexpr (NP == 0) {
+        if constexpr (FPRO) {
+#pragma unroll
+            for (int k = 0; k < UM; ++k) {
+                const int un = min(k * NT + tid, nunits - 1);
+                const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
+                xv[k][0] = xp[0]; xv[k][1] = xp[1];
+                if constexpr (PRO == PRO_NORM) {
+                    const float4 * gp = (const float4 *) (P.g + (size_t) un * 8);
+                    gv[k][0] = gp[0]; gv[k][1] = gp[1];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < UM; ++k) {
+                const int b = min(k * NT + tid, nb - 1);
+                qv[k] = P.xq.qs[b];
+                dv[k] = P.xq.d[b];
+            }
+        }
+    }
+
+    // first D chunks of this wave's first row group (wave-uniform base +
+    // 32-bit lane offset: the scalar-base load form).  A wave without row
+    // groups (NP == 0 only) aims its loads at one 16-byte word.
+    const uint32_t loff = ng > 0 ? (uint32_t) lane * 16u : 0u;
+    uint4 W[D][4];
+    float4 S[D];
+#define LVK_ISSUE(slot, grp, cc)                                                                        \
+    do {                                                                                                \
+        const uint4 * nb_ = P.nib + ((size_t) (grp) * NC * 4 + (cc) * 4) * 64;                          \
+        _Pragma("unroll") for (int sb = 0; sb < 4; ++sb) if ((cc) * 4 + sb < nsub)                      \
+            W[slot][sb] = ld_nt((const uint4 *) ((const char *) (nb_ + sb * 64) + loff));               \
+        S[slot] = *(const float4 *) ((const char *) (P.scl + ((size_t) (grp) * NC + (cc)) * 64) + loff); \
+        __builtin_amdgcn_sched_barrier(0);                                                              \
+    } while (0)
+#pragma unroll
+    for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
+
+    if constexpr (NP == 0) {
+        double * red = (double *) (sbuf + NW * 512);     // NW doubles (after the s buffers)
+        if constexpr (FPRO) {
+            float scale = 1.0f;
+            if constexpr (PRO == PRO_NORM) {
+                // ggml_compute_forward_rms_norm_f32 (ggml.c:6058-6076): float
+                // squares summed in double; per-thread units, a DPP wave tree,
+                // then the NW wave sums in order (RMSNorm order)
+                double acc = 0.0;
+#pragma unroll
+                for (int k = 0; k < UM; ++k) {
+                    if (k * NT + tid < nunits) {
+                        const float e[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
+                                            xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) { const float sq = e[q] * e[q]; acc += (double) sq; }
+                    }
+                }
+                acc = wave_sum_d(acc);
+                if (lane == 0) red[wave] = acc;
+                __syncthreads();
+                double sum = red[0];
+                for (int w = 1; w < NW; ++w) sum += red[w];
+                const float mean = (float) (sum / (double) KT);
+                scale = 1.0f / sqrtf(mean + 1e-6f);
+            }
+#pragma unroll
+            for (int k = 0; k < UM; ++k) {
+                if (k * NT >= nunits) break;
+                const int un = k * NT + tid;
+                float v[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
+                              xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
+                float amax = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if constexpr (PRO == PRO_NORM) {
+                        const float gg[8] = {gv[k][0].x, gv[k][0].y, gv[k][0].z, gv[k][0].w,
+                                             gv[k][1].x, gv[k][1].y, gv[k][1].z, gv[k][1].w};
+                        const float yn = v[e] * scale;      // ggml_vec_scale_f32 (ggml.c:6076)
+                        v[e] = gg[e] * yn;                  // ggml_mul(repeat(g), cur) (llama.cpp:984)
+                    }
+                    const float a = fabsf(v[e]);
+                    amax = a > amax ? a : amax;
+                }
+                const float o0 = quad_bcast<0>(amax), o1 = quad_bcast<1>(amax);
+                const float o2 = quad_bcast<2>(amax), o3 = quad_bcast<3>(amax);
+                const float m01 = o1 > o0 ? o1 : o0, m23 = o3 > o2 ? o3 : o2;
+                amax = m23 > m01 ? m23 : m01;
+                const float d = amax / 7.0f;                              // ggml.c:651
+                const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;     // ggml.c:653
+                const uint32_t w = q40_pack8(v, id);
+                if (un < nunits) act_store(act, dxp, un >> 2, un & 3, w, d, (un & 3) == 0);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < UM; ++k) {
+                const int b = k * NT + tid;
+                if (b < nb) {
+                    act_store(act, dxp, b, 0, qv[k].x, dv[k], true);
+                    act_store(act, dxp, b, 1, qv[k].y, 0.0f, false);
+                    act_store(act, dxp, b, 2, qv[k].z, 0.0f, false);
+                    act_store(act, dxp, b, 3, qv[k].w, 0.0f, false);
+                }
+            }
+        }
+    }
+    LVK_T(1);
+    __syncthreads();            // activation table ready
+    LVK_T(2);
+    if (NP == 0 && ng == 0) return;
+
+    // 4. row groups: chunk loop with cross-group prefetch
+    float * sw = sbuf + wave * 2 * 256;
+    auto body = [&](auto has_next, int grp, int gnext) __attribute__((always_inline)) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int slot = c % D;
+            LVK_T(tq); ++tq;
+#ifdef LVK_PROBE_NOCOMPUTE   // dev probe builds only: consume the weights trivially
+            acc += __uint_as_float(W[slot][0].x ^ W[slot][nsub > 1 ? 1 : 0].y) * S[slot].x;
+            if (false) {
+#else
+            {
+#endif
+            float * sl = sw + (c & 1) * 256;
+            // s = dw * dx of blocks 32c + 8m + j of row r (ggml.c:1968)
+            const float4 dx = *(const float4 *) (dxp + c * 32 + j * 4);
+            float4 sv;
+            sv.x = S[slot].x * dx.x; sv.y = S[slot].y * dx.y; sv.z = S[slot].z * dx.z; sv.w = S[slot].w * dx.w;
+            *(float4 *) (sl + r * 32 + j * 4) = sv;
+            __builtin_amdgcn_wave_barrier();
+            float sa[8][4];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const float4 v = *(const float4 *) (sl + r * 32 + jj * 4);
+                sa[jj][0] = v.x; sa[jj][1] = v.y; sa[jj][2] = v.z; sa[jj][3] = v.w;
+            }
+#pragma unroll
+            for (int sb = 0; sb < 4; ++sb) {
+                if (c * 4 + sb < nsub) {
+                    const uint32_t wd[4] = {W[slot][sb].x, W[slot][sb].y, W[slot][sb].z, W[slot][sb].w};
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp) {
+                        const int bi = sb * 8 + pp * 4;
+                        const uint4 a = *(const uint4 *) (act + ((c * 8 + sb * 2 + pp) * 8 + j) * 4);
+                        const int p0 = dot8(wd[2 * pp], a.x);
+                        const int p1 = dot8(wd[2 * pp], a.y);
+                        const int p2 = dot8(wd[2 * pp + 1], a.z);
+                        const int p3 = dot8(wd[2 * pp + 1], a.w);
+                        acc = __builtin_fmaf(sa[(bi + 0) & 7][(bi + 0) >> 3], (float) p0, acc);
+                        acc = __builtin_fmaf(sa[(bi + 1) & 7][(bi + 1) >> 3], (float) p1, acc);
+                        acc = __builtin_fmaf(sa[(bi + 2) & 7][(bi + 2) >> 3], (float) p2, acc);
+                        acc = __builtin_fmaf(sa[(bi + 3) & 7][(bi + 3) >> 3], (float) p3, acc);
+                    }
+                }
+            }
+            }
+            if (c + D < NC) LVK_ISSUE(slot, grp, c + D);
+            else if constexpr (decltype(has_next)::value && XG) LVK_ISSUE(slot, gnext, c + D - NC);
+            // keep chunks in program order: the chain value is pinned here, so
+            // chunk c's arithmetic cannot sink below chunk c+1's reads
+            asm volatile("" : "+v"(acc));
+            LVK_T(tq); ++tq;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return octet_reduce(acc);
+    };
+
+    auto epilogue = [&](int grp, float res) __attribute__((always_inline)) {
+        const int row = grp * 8 + r;
+        if constexpr (EPI == EPI_STORE) {
+            if (j == 0) P.y[row] = res;
+        } else if constexpr (EPI == EPI_RESID) {
+            if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+        } else if constexpr (EPI == EPI_QKV) {
+            const int E = P.n_embd, hd = P.head_dim;
+            const int which = row / E;          // 0 q, 1 k, 2 v (uniform per wave: E % 8 == 0)
+            const int e = row - which * E;
+            const int pos = P.sp->n_past;
+            const float other = __shfl_xor(res, 8);   // row e^1 lives in lanes of row r^1
+            if (j == 0) {
+                if (which < 2) {
+                    // ggml_compute_forward_rope_f32 mode 0 (ggml.c:7209-7223)
+                    const int i0 = e % hd;
+                    const float2 cs = P.rope[(size_t) pos * (hd / 2) + (i0 >> 1)];
+                    float out;
+                    if ((i0 & 1) == 0) { const float a = res * cs.x, b = other * cs.y; out = a - b; }
+                    else               { const float a = other * cs.y, b = res * cs.x; out = a + b; }
+                    if (which == 0) P.q16[e] = f32_to_f16(out);
+                    else            P.kc[(size_t) pos * E + e] = f32_to_f16(out);
+                } else {
+                    P.vc[(size_t) e * P.n_ctx + pos] = f32_to_f16(res);
+                }
+            }
+        } else if constexpr (EPI == EPI_SWIGLU_F32) {
+            // fused W1|W3 image interleaved per 4 rows: rows 0-3 of the group are
+            // w1 rows 4grp..4grp+3, rows 4-7 the w3 rows (llama.cpp:1085-1096)
+            const float a3 = __shfl_xor(res, 32);
+            if (r < 4 && j == 0) {
+                const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res)]);   // ggml_vec_silu_f32 (ggml.c:2495)
+                P.u[grp * 4 + r] = sl * a3;                                  // ggml_mul (llama.cpp:1096)
+            }
+        }
+    };
+
+    if constexpr (XG) {
+        for (int k = 0; k + 1 < ng; ++k) {
+            const float res = body(std::true_type{}, gc, gc + NW);
+            epilogue(gc, res);
+            gc += NW;
+        }
+    }
+    const float res = body(std::false_type{}, gc, gc);
+    epilogue(gc, res);
+    LVK_T(3);
+#undef LVK_ISSUE
+}
+
+// -- host -------------------------------------------------------------------
+
+int cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return 256;
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 256;
+        n = p.multiProcessorCount;
+    }
+    return n;
+}
+
+template <int NW, int NP, int D, int PRO, int EPI, int KT>
+hipError_t go(const CuParams & P, hipStream_t s) {
+    constexpr int nb = KT / 32, NC = (nb + 31) / 32;
+    constexpr bool XG = (NC % D) == 0;
+    const int nwg = std::min(cu_count(), P.G);
+    // without cross-group prefetch every wave must own at most one group
+    if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
+    const size_t lds = (size_t) nb * 32 + NC * 128 + NW * 2 * 1024 + NW * 8;
+    LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+#ifdef LVK_PROBE_TIMING
+void * lvk_probe_trace() { void * p = nullptr; (void) hipGetSymbolAddress(&p, HIP_SYMBOL(g_trace)); return p; }
+#endif
+bool matvec_cu_supported(int K) { return K == 4096 || K == 11008; }
+
+hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s) {
+    if (L.w.qtype != Q4_0 || L.n_tokens != 1 || L.w.M % 8) return hipErrorNotSupported;
+    CuParams P{};
+    P.nib = L.w.nib;
+    P.scl = (const float4 *) L.w.scl;
+    P.G = L.w.M / 8;
+    P.x = L.x + (size_t) L.tok0 * L.w.K;
+    P.g = L.g;
+    P.xq = L.xq;
+    if (P.xq.qs) { P.xq.qs += (size_t) L.tok0 * L.xq.nb; P.xq.d += (size_t) L.tok0 * L.xq.nb; }
+    P.sp = L.sp;
+    P.y = L.y ? L.y + (size_t) L.out_tok0 * L.w.M : nullptr;
+    P.u = L.u;
+    P.q16 = L.q16; P.kc = L.kc; P.vc = L.vc; P.rope = L.rope.cs;
+    P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx;
+    P.silu_tab = L.silu_tab;
+    const int K = L.w.K;
+#ifdef LVK_PROBE_SWEEP   // dev probe builds only: LVK_CFG selects a launch shape
+    {
+        static int cfg = getenv("LVK_CFG") ? atoi(getenv("LVK_CFG")) : 0;
+#define SW4(E, PR, K_, a0, a1, a2, a3)                                                          \
+        switch (cfg) { case 0: return go<a0, PR, E, K_>(P, s); case 1: return go<a1, PR, E, K_>(P, s); \
+                       case 2: return go<a2, PR, E, K_>(P, s); default: return go<a3, PR, E, K_>(P, s); }
+#define C3(a, b, c) a, b, c
+        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(6, 0, 4), C3(12, 0, 2), C3(6, 2, 4))
+        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(8, 0, 4), C3(10, 0, 2), C3(8, 4, 2))
+        if (K == 4096 && epi == EPI_STORE) SW4(EPI_STORE, PRO_NORM, 4096, C3(16, 0, 2), C3(8, 0, 4), C3(12, 0, 2), C3(8, 4, 2))
+        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 0, 4), C3(2, 2, 2), C3(4, 0, 2))
+        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(2, 2, 6), C3(2, 4, 4), C3(4, 0, 4), C3(2, 6, 6))
+    }
+#endif
+    if (K == 4096) {
+        switch (epi) {
+            case EPI_QKV: if (pro == PRO_NORM) return go<8, 0, 2, PRO_NORM, EPI_QKV, 4096>(P, s); break;
+            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 4096>(P, s); break;
+            case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 4096>(P, s); break;
+            case EPI_RESID: if (pro == PRO_ACTQ) return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096>(P, s); break;
+        }
+    } else if (K == 11008) {
+        if (epi == EPI_RESID && pro == PRO_ACTF) return go<4, 0, 4, PRO_ACTF, EPI_RESID, 11008>(P, s);
+    }
+    return hipErrorNotSupported;
+}
+
+}  // namespace lvk

@@ -4,6 +4,7 @@
 #include "lvk_kernels.h"
 
 namespace lvk {
+thread_local LaunchEvents g_launch_events;
 
 namespace {
 
@@ -36,44 +37,45 @@ __global__ void k_embed(const uint8_t * __restrict__ emb, int type, int E, const
     x[(size_t) t * E + e] = v;
 }
 
-// Q4_0 file rows -> quad-sliced image.  One thread per (row, chunk of 8 blocks).
-//   G(i,j) = (qs_i[2j] | qs_i[2j+1] << 8) ^ 0x8888   (elements 4j..4j+3, signed)
-//   X(i,q) = G(i,2q)   | G(i+1,2q)   << 16
-//   Y(i,q) = G(i,2q+1) | G(i+1,2q+1) << 16
-//   nib[g][c][h][4r+q] = {X(8c+4h,q), Y(8c+4h,q), X(8c+4h+2,q), Y(8c+4h+2,q)}
-//   scl[g][c][4r+q]    = {d(8c+q), d(8c+4+q)}
+// Q4_0 file rows -> octet image (matvec_q4.hip).  One thread per
+// (row, 32-block chunk c, chain j):
+//   a(i,j)  = (qs_i[2j] | qs_i[2j+1] << 8) ^ 0x8888   (elements 4j..4j+3, signed)
+//   W(p,j)  = a(2p,j) | a(2p+1,j) << 16              (block pair p)
+//   nib[g][c][sb][8r+j] = {W(16c+4sb+k, j), k = 0..3}  (blocks 32c+8sb .. +7)
+//   scl[g][c][8r+j]     = {d(32c+8m+j), m = 0..3}
+// Sub-chunks / blocks past the row end are zero (never consumed).
 __global__ void k_repack_q40(const uint8_t * __restrict__ src, int M, int K, uint4 * __restrict__ nib,
-                             float2 * __restrict__ scl) {
-    const int nb = K / 32, C = K / 256;
+                             float4 * __restrict__ scl, int il4) {
+    const int nb = K / 32, NC = (nb + 31) / 32;
     const long idx = (long) blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long) M * C) return;
-    const int row = (int) (idx / C), c = (int) (idx % C);
-    const int g = row / 16, r = row % 16;
-    const uint8_t * rb = src + (size_t) row * nb * 20;
-    float d[8];
-    uint32_t G[8][8];   // [block k][group j]
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint8_t * b = rb + (size_t) (c * 8 + k) * 20;
-        d[k] = *(const float *) b;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) G[k][j] = ((uint32_t) b[4 + 2 * j] | ((uint32_t) b[5 + 2 * j] << 8)) ^ 0x8888u;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int lane = 4 * r + q;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int i0 = 4 * h, i1 = 4 * h + 2;
-            uint4 v;
-            v.x = G[i0][2 * q] | (G[i0 + 1][2 * q] << 16);
-            v.y = G[i0][2 * q + 1] | (G[i0 + 1][2 * q + 1] << 16);
-            v.z = G[i1][2 * q] | (G[i1 + 1][2 * q] << 16);
-            v.w = G[i1][2 * q + 1] | (G[i1 + 1][2 * q + 1] << 16);
-            nib[(((size_t) g * C + c) * 2 + h) * 64 + lane] = v;
+    if (idx >= (long) M * NC * 8) return;
+    const int j = (int) (idx & 7);
+    const long rc = idx >> 3;
+    const int row = (int) (rc / NC), c = (int) (rc % NC);
+    const int g = row / 8, r = row % 8;
+    const int lane = 8 * r + j;
+    // il4: src holds two M/2-row matrices [A; B], fused per 4 rows (A0-3 B0-3 A4-7 ...)
+    const int srow = il4 ? ((row & 7) < 4 ? (row >> 3) * 4 + (row & 7) : M / 2 + (row >> 3) * 4 + (row & 7) - 4) : row;
+    const uint8_t * rb = src + (size_t) srow * nb * 20;
+    auto grp = [&](int i) -> uint32_t {
+        if (i >= nb) return 0u;
+        const uint8_t * b = rb + (size_t) i * 20;
+        return ((uint32_t) b[4 + 2 * j] | ((uint32_t) b[5 + 2 * j] << 8)) ^ 0x8888u;
+    };
+    for (int sb = 0; sb < 4; ++sb) {
+        uint32_t w[4];
+        for (int k = 0; k < 4; ++k) {
+            const int i = 32 * c + 8 * sb + 2 * k;
+            w[k] = (i < nb) ? (grp(i) | (grp(i + 1) << 16)) : 0u;
         }
-        scl[((size_t) g * C + c) * 64 + lane] = make_float2(d[q], d[4 + q]);
+        nib[(((size_t) g * NC + c) * 4 + sb) * 64 + lane] = make_uint4(w[0], w[1], w[2], w[3]);
     }
+    float d[4];
+    for (int m = 0; m < 4; ++m) {
+        const int i = 32 * c + 8 * m + j;
+        d[m] = (i < nb) ? *(const float *) (rb + (size_t) i * 20) : 0.0f;
+    }
+    scl[((size_t) g * NC + c) * 64 + lane] = make_float4(d[0], d[1], d[2], d[3]);
 }
 
 // standalone activation quantizer (quantize_row_q4_0 AVX2, ggml.c:621-685)
@@ -105,16 +107,17 @@ __global__ void k_quantize_q40(const float * __restrict__ x, int N, int K, ActQ 
 hipError_t launch_embed(const void * emb, int emb_type, int n_embd, const int * tokens, int n, float * x,
                         hipStream_t s) {
     dim3 grid((n_embd + 255) / 256, n);
-    hipLaunchKernelGGL(k_embed, grid, dim3(256), 0, s, (const uint8_t *) emb, emb_type, n_embd, tokens, x);
+    LVK_LAUNCH(k_embed, grid, dim3(256), 0, s, (const uint8_t *) emb, emb_type, n_embd, tokens, x);
     return hipGetLastError();
 }
 
-hipError_t launch_repack(const void * src_rows, int qtype, int M, int K, uint4 * nib, void * scl, hipStream_t s) {
-    if (M % 16 || K % 256) return hipErrorInvalidValue;
-    const long n = (long) M * (K / 256);
+hipError_t launch_repack(const void * src_rows, int qtype, int M, int K, uint4 * nib, void * scl, hipStream_t s,
+                         int interleave4) {
+    if (M % 8 || K % 256) return hipErrorInvalidValue;
+    const long n = (long) M * ((K / 32 + 31) / 32) * 8;
     if (qtype == Q4_0) {
         hipLaunchKernelGGL(k_repack_q40, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s,
-                           (const uint8_t *) src_rows, M, K, nib, (float2 *) scl);
+                           (const uint8_t *) src_rows, M, K, nib, (float4 *) scl, interleave4);
         return hipGetLastError();
     }
     return hipErrorNotSupported;

@@ -75,6 +75,7 @@ void Context::init(const llama_context_params & p) {
     aq_ffn.d = (float *) model.alloc(C * (F / 32) * 4);
     aq_ffn.m = (float *) model.alloc(C * (F / 32) * 4);
     aq_ffn.qs = (uint4 *) model.alloc(C * (F / 32) * 16);
+    u_ffn = (float *) model.alloc(F * 4);
     logits_d = (float *) model.alloc(C * V * 4);
     emb_d = (float *) model.alloc(E * 4);
     sp_d = (StepParams *) model.alloc(sizeof(StepParams));
@@ -120,9 +121,10 @@ void Context::timed_launch(int cls, double bytes, const std::function<hipError_t
     auto & e = ev_pool[ev_used];
     ev_class[ev_used] = cls;
     ++ev_used;
-    LVK_HIP(hipEventRecord(e.first, stream));
-    LVK_HIP(fn());
-    LVK_HIP(hipEventRecord(e.second, stream));
+    g_launch_events = {e.first, e.second};
+    const hipError_t err = fn();
+    g_launch_events = {};
+    LVK_HIP(err);
     prof.launches[cls] += 1;
     prof.bytes[cls] += bytes;
 }
@@ -138,11 +140,22 @@ void Context::collect_profile() {
 
 static double qbytes(const QMatrix & w) { return (double) w.M * (w.K / 32) * (w.qtype == Q4_0 ? 20 : 24); }
 
+// decode kernels: the CU-balanced path (matvec_cu.hip) where its row length is
+// compiled in, else the generic kernel
+static hipError_t mv_launch(const MvLaunch & L, int pro, int epi, hipStream_t s) {
+    if (L.n_tokens == 1 && matvec_cu_supported(L.w.K)) {
+        const hipError_t e = launch_matvec_cu(L, pro, epi, s);
+        if (e != hipErrorNotSupported) return e;
+    }
+    return launch_matvec(L, pro, epi, s);
+}
+
 void Context::enqueue_forward(int n, bool last_only) {
     const HParams & hp = model.hp;
-    const int E = (int) hp.n_embd, H = (int) hp.n_head, hd = E / H, V = (int) hp.n_vocab;
-    (void) V;
+    const int E = (int) hp.n_embd, H = (int) hp.n_head, hd = E / H, F = (int) hp.n_ff();
     const size_t CE = (size_t) n_ctx * E;
+    // single-token FFN: W1|W3 hands silu(w1 x)*(w3 x) to W2 in f32, W2 quantizes it
+    const bool ffn_f32 = n == 1 && model.qtype == Q4_0 && matvec_cu_supported(E) && matvec_cu_supported(F);
     timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_d, n, x, stream); });
     for (size_t il = 0; il < model.layers.size(); ++il) {
         const Layer & ly = model.layers[il];
@@ -150,24 +163,30 @@ void Context::enqueue_forward(int n, bool last_only) {
         a.w = ly.wqkv; a.x = x; a.g = ly.attn_norm; a.sp = sp_d; a.n_tokens = n;
         a.q16 = q16; a.kc = kc + il * CE; a.vc = vc + il * CE; a.rope.cs = rope;
         a.n_embd = E; a.head_dim = hd; a.n_ctx = n_ctx;
-        timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return launch_matvec(a, PRO_NORM, EPI_QKV, stream); });
+        timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
         AttnLaunch at{q16, kc + il * CE, vc + il * CE, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
         timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
         MvLaunch b;
         b.w = ly.wo; b.xq = aq_attn; b.y = x; b.sp = sp_d; b.n_tokens = n;
-        timed_launch(K_WO, qbytes(ly.wo), [&] { return launch_matvec(b, PRO_ACTQ, EPI_RESID, stream); });
+        timed_launch(K_WO, qbytes(ly.wo), [&] { return mv_launch(b, PRO_ACTQ, EPI_RESID, stream); });
         MvLaunch c;
-        c.w = ly.w13; c.x = x; c.g = ly.ffn_norm; c.sp = sp_d; c.n_tokens = n; c.silu_tab = silu_tab; c.out_q = aq_ffn;
-        timed_launch(K_W13, qbytes(ly.w13), [&] { return launch_matvec(c, PRO_NORM, EPI_SWIGLU, stream); });
+        c.w = ly.w13; c.x = x; c.g = ly.ffn_norm; c.sp = sp_d; c.n_tokens = n; c.silu_tab = silu_tab;
+        c.out_q = aq_ffn; c.u = u_ffn;
         MvLaunch d;
-        d.w = ly.w2; d.xq = aq_ffn; d.y = x; d.sp = sp_d; d.n_tokens = n;
-        timed_launch(K_W2, qbytes(ly.w2), [&] { return launch_matvec(d, PRO_ACTQ, EPI_RESID, stream); });
+        d.w = ly.w2; d.xq = aq_ffn; d.x = u_ffn; d.y = x; d.sp = sp_d; d.n_tokens = n;
+        if (ffn_f32) {
+            timed_launch(K_W13, qbytes(ly.w13), [&] { return launch_matvec_cu(c, PRO_NORM, EPI_SWIGLU_F32, stream); });
+            timed_launch(K_W2, qbytes(ly.w2), [&] { return launch_matvec_cu(d, PRO_ACTF, EPI_RESID, stream); });
+        } else {
+            timed_launch(K_W13, qbytes(ly.w13), [&] { return launch_matvec(c, PRO_NORM, EPI_SWIGLU, stream); });
+            timed_launch(K_W2, qbytes(ly.w2), [&] { return launch_matvec(d, PRO_ACTQ, EPI_RESID, stream); });
+        }
     }
     MvLaunch o;
     o.w = model.output; o.x = x; o.g = model.norm; o.sp = sp_d; o.y = logits_d;
     o.tok0 = last_only ? n - 1 : 0;
     o.n_tokens = last_only ? 1 : n;
-    timed_launch(K_LMHEAD, qbytes(model.output), [&] { return launch_matvec(o, PRO_NORM, EPI_STORE, stream); });
+    timed_launch(K_LMHEAD, qbytes(model.output), [&] { return mv_launch(o, PRO_NORM, EPI_STORE, stream); });
     if (want_embedding)
         LVK_HIP(launch_rmsnorm_rows(x + (size_t) (n - 1) * E, model.norm, E, 1, emb_d, stream));
 }

@@ -35,6 +35,7 @@ struct Context {
     float * scores = nullptr;    // [n_ctx][H][n_ctx]
     ActQ aq_attn;                // [n_ctx][E/32]
     ActQ aq_ffn;                 // [n_ctx][F/32]
+    float * u_ffn = nullptr;     // [F] decode: silu(w1 x) * (w3 x) in f32
     float * logits_d = nullptr;  // [n_ctx][V]
     float * emb_d = nullptr;     // [E]
     uint16_t * exp_tab = nullptr;

@@ -10,7 +10,7 @@
 //
 // Upload: each layer matrix is copied into a device staging buffer (fused
 // matrices assembled there: wq|wk|wv rows, and w1/w3 interleaved per 32-row
-// block) and repacked on the GPU into the quad-sliced image the matvec
+// block) and repacked on the GPU into the octet image the matvec
 // streams (lvk_kernels.h QMatrix).  The image has exactly the file's bytes.
 #include "lvk_model.h"
 
@@ -253,15 +253,15 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
     auto make_matrix = [&](int M, int K) -> QMatrix {
         QMatrix q;
         q.qtype = m.qtype; q.M = M; q.K = K;
-        const size_t nib = (size_t) M * (K / 32) * 16;               // 16 B of nibbles per block
-        const size_t scl = (size_t) M * (K / 32) * (m.qtype == Q4_0 ? 4 : 8);
+        const size_t nib = qimage_nib_bytes(M, K);
+        const size_t scl = qimage_scl_bytes(M, K);
         q.nib = (const uint4 *) m.alloc(nib);
         q.scl = m.alloc(scl);
-        m.weight_bytes += nib + scl;
+        m.weight_bytes += (size_t) M * (K / 32) * (m.qtype == Q4_0 ? 20 : 24);
         return q;
     };
-    auto repack = [&](QMatrix & q) {
-        LVK_HIP(launch_repack(stage, q.qtype, q.M, q.K, (uint4 *) q.nib, (void *) q.scl, s));
+    auto repack = [&](QMatrix & q, int interleave4 = 0) {
+        LVK_HIP(launch_repack(stage, q.qtype, q.M, q.K, (uint4 *) q.nib, (void *) q.scl, s, interleave4));
         LVK_HIP(hipStreamSynchronize(s));
     };
     auto check_q = [&](const Tensor & t, const std::string & name) {
@@ -313,12 +313,12 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
         ly.wo = make_matrix((int) E, (int) E);
         repack(ly.wo);
         tick(wo.size);
-        // fused W1|W3, interleaved per 32 output rows
-        const size_t blk = 32 * rb_E;
-        LVK_HIP(hipMemcpy2D(st, 2 * blk, w1.host, blk, blk, F / 32, hipMemcpyHostToDevice));
-        LVK_HIP(hipMemcpy2D(st + blk, 2 * blk, w3.host, blk, blk, F / 32, hipMemcpyHostToDevice));
+        // fused W1|W3, interleaved per 4 output rows by the repack (a row group
+        // of 8 holds w1 and w3 rows of the same 4 outputs: SwiGLU stays in a wave)
+        LVK_HIP(hipMemcpy(st, w1.host, w1.size, hipMemcpyHostToDevice));
+        LVK_HIP(hipMemcpy(st + w1.size, w3.host, w3.size, hipMemcpyHostToDevice));
         ly.w13 = make_matrix(2 * (int) F, (int) E);
-        repack(ly.w13);
+        repack(ly.w13, 1);
         tick(2 * w1.size);
         LVK_HIP(hipMemcpy(stage, w2.host, w2.size, hipMemcpyHostToDevice));
         ly.w2 = make_matrix((int) E, (int) F);

@@ -81,14 +81,14 @@ int lvk_quantize_rows(int type, const float * x, int n, int k, void * y) {
 
 static int mul_mat_impl(int type, const void * w, int m, int k, const float * g, const float * x, int n, float * y,
                         bool norm) {
-    if (m % 16 || k % 256) return fail("lvk_mul_mat_q", "need m % 16 == 0 and k % 256 == 0");
+    if (m % 8 || k % 256) return fail("lvk_mul_mat_q", "need m % 8 == 0 and k % 256 == 0");
     Dev dv;
     const size_t nb = (size_t) k / 32, bb = block_bytes(type);
     void * wd = dv.up((const uint8_t *) w, (size_t) m * nb * bb);
     lvk::QMatrix q;
     q.qtype = type; q.M = m; q.K = k;
-    q.nib = (const uint4 *) dv.get((size_t) m * nb * 16);
-    q.scl = dv.get((size_t) m * nb * (type == lvk::Q4_0 ? 4 : 8));
+    q.nib = (const uint4 *) dv.get(lvk::qimage_nib_bytes(m, k));
+    q.scl = dv.get(lvk::qimage_scl_bytes(m, k));
     LVK_HIP(lvk::launch_repack(wd, type, m, k, (uint4 *) q.nib, (void *) q.scl, nullptr));
     lvk::StepParams sp{0, n, 0, 0};
     lvk::StepParams * spd = dv.up(&sp, 1);

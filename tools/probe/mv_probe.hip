@@ -1,0 +1,181 @@
+// mv_probe: times the decode kernels of llama.vk_amd on one synthetic 7B Q4_0 token
+// (32 layers of distinct weight images, so nothing is served from the 256 MiB MALL)
+// and compares with the pure weight-stream floor measured by bw_probe.
+// Build: make -C tools/probe ; run on the GPU box.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "lvk_kernels.h"
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1);} } while (0)
+using namespace lvk;
+#ifdef LVK_PROBE_TIMING
+namespace lvk { void * lvk_probe_trace(); }
+#endif
+
+__global__ void k_fill_u32(uint32_t * p, size_t n, uint32_t seed) {
+    for (size_t i = blockIdx.x * (size_t) blockDim.x + threadIdx.x; i < n; i += (size_t) gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t) i * 2654435761u ^ seed; h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+        p[i] = h;
+    }
+}
+__global__ void k_fill_f32(float * p, size_t n, float lo, float hi, uint32_t seed) {
+    for (size_t i = blockIdx.x * (size_t) blockDim.x + threadIdx.x; i < n; i += (size_t) gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t) i * 2654435761u ^ seed; h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+        p[i] = lo + (hi - lo) * (h & 0xFFFFFF) / 16777216.0f;
+    }
+}
+__global__ void k_fill_f16(uint16_t * p, size_t n, uint32_t seed) {
+    for (size_t i = blockIdx.x * (size_t) blockDim.x + threadIdx.x; i < n; i += (size_t) gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t) i * 2654435761u ^ seed; h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+        p[i] = (uint16_t) (0x2C00 + (h & 0x3FF)) | (uint16_t) ((h >> 16) & 0x8000);
+    }
+}
+static void fill_u32(void * p, size_t bytes, uint32_t seed) { hipLaunchKernelGGL(k_fill_u32, dim3(1024), dim3(256), 0, 0, (uint32_t *) p, bytes / 4, seed); }
+static void fill_f32(void * p, size_t n, float lo, float hi, uint32_t seed) { hipLaunchKernelGGL(k_fill_f32, dim3(1024), dim3(256), 0, 0, (float *) p, n, lo, hi, seed); }
+static void * dalloc(size_t b) { void * p; CK(hipMalloc(&p, b + 4096)); return p; }
+
+static QMatrix mkmat(int M, int K, uint32_t seed) {
+    QMatrix q; q.qtype = Q4_0; q.M = M; q.K = K;
+    size_t nb = qimage_nib_bytes(M, K), sb = qimage_scl_bytes(M, K);
+    void * n = dalloc(nb); void * s = dalloc(sb);
+    fill_u32(n, nb, seed); fill_f32(s, sb / 4, 0.001f, 0.01f, seed + 1);
+    q.nib = (const uint4 *) n; q.scl = s;
+    return q;
+}
+
+int main(int argc, char ** argv) {
+    const int E = 4096, F = 11008, H = 32, L = 32, V = 32000, C = 512, hd = 128;
+    const int n_past = argc > 1 ? atoi(argv[1]) : 256;
+    struct Lay { QMatrix qkv, wo, w13, w2; };
+    std::vector<Lay> ly(L);
+    for (int l = 0; l < L; l++) {
+        ly[l].qkv = mkmat(3 * E, E, 100 * l + 1); ly[l].wo = mkmat(E, E, 100 * l + 2);
+        ly[l].w13 = mkmat(2 * F, E, 100 * l + 3); ly[l].w2 = mkmat(E, F, 100 * l + 4);
+    }
+    QMatrix lm = mkmat(V, E, 7);
+    float * x = (float *) dalloc(E * 4); fill_f32(x, E, -1.f, 1.f, 11);
+    float * g = (float *) dalloc(E * 4); fill_f32(g, E, 0.9f, 1.1f, 12);
+    uint16_t * q16 = (uint16_t *) dalloc(E * 2);
+    uint16_t * kc = (uint16_t *) dalloc((size_t) L * C * E * 2); uint16_t * vc = (uint16_t *) dalloc((size_t) L * C * E * 2);
+    hipLaunchKernelGGL(k_fill_f16, dim3(1024), dim3(256), 0, 0, kc, (size_t) L * C * E, 5u);
+    hipLaunchKernelGGL(k_fill_f16, dim3(1024), dim3(256), 0, 0, vc, (size_t) L * C * E, 6u);
+    float * scores = (float *) dalloc((size_t) H * C * 4);
+    ActQ aqa; aqa.nb = E / 32; aqa.d = (float *) dalloc(E / 32 * 4); aqa.m = (float *) dalloc(E / 32 * 4); aqa.qs = (uint4 *) dalloc(E / 32 * 16);
+    ActQ aqf; aqf.nb = F / 32; aqf.d = (float *) dalloc(F / 32 * 4); aqf.m = (float *) dalloc(F / 32 * 4); aqf.qs = (uint4 *) dalloc(F / 32 * 16);
+    fill_f32(aqa.d, E / 32, 0.01f, 0.1f, 13); fill_u32(aqa.qs, E / 32 * 16, 14);
+    fill_f32(aqf.d, F / 32, 0.01f, 0.1f, 15); fill_u32(aqf.qs, F / 32 * 16, 16);
+    float * logits = (float *) dalloc((size_t) V * 4);
+    float2 * rope = (float2 *) dalloc((size_t) C * hd / 2 * 8); fill_f32(rope, (size_t) C * hd, -1.f, 1.f, 17);
+    uint16_t * etab = (uint16_t *) dalloc(65536 * 2); uint16_t * stab = (uint16_t *) dalloc(65536 * 2);
+    hipLaunchKernelGGL(k_fill_f16, dim3(256), dim3(256), 0, 0, etab, 65536, 8u);
+    hipLaunchKernelGGL(k_fill_f16, dim3(256), dim3(256), 0, 0, stab, 65536, 9u);
+    StepParams sph{n_past, 1, 0, 0};
+    StepParams * sp = (StepParams *) dalloc(16); CK(hipMemcpy(sp, &sph, 16, hipMemcpyHostToDevice));
+    CK(hipDeviceSynchronize());
+    hipStream_t s; CK(hipStreamCreate(&s));
+
+    float * u = (float *) dalloc(F * 4); fill_f32(u, F, -1.f, 1.f, 18);
+    const bool cu = getenv("LVK_PROBE_GENERIC") == nullptr;
+    auto mv = [&](const MvLaunch & L, int pro, int epi) {
+        if (cu) { hipError_t e = launch_matvec_cu(L, pro, epi, s); if (e != hipErrorNotSupported) return e; }
+        return launch_matvec(L, pro, epi, s);
+    };
+    auto op = [&](int k, int l) {
+        const Lay & y = ly[l];
+        if (k == 0) {
+            MvLaunch a; a.w = y.qkv; a.x = x; a.g = g; a.sp = sp; a.n_tokens = 1; a.q16 = q16;
+            a.kc = kc + (size_t) l * C * E; a.vc = vc + (size_t) l * C * E; a.rope.cs = rope; a.n_embd = E; a.head_dim = hd; a.n_ctx = C;
+            CK(mv(a, PRO_NORM, EPI_QKV));
+        } else if (k == 1) {
+            AttnLaunch at{q16, kc + (size_t) l * C * E, vc + (size_t) l * C * E, scores, aqa, Q4_0, etab, sp, 1, E, H, C};
+            CK(launch_attention(at, s));
+        } else if (k == 2) {
+            MvLaunch b; b.w = y.wo; b.xq = aqa; b.y = x; b.sp = sp; b.n_tokens = 1;
+            CK(mv(b, PRO_ACTQ, EPI_RESID));
+        } else if (k == 3) {
+            MvLaunch c; c.w = y.w13; c.x = x; c.g = g; c.sp = sp; c.n_tokens = 1; c.silu_tab = stab; c.out_q = aqf; c.u = u;
+            if (cu) CK(launch_matvec_cu(c, PRO_NORM, EPI_SWIGLU_F32, s)); else CK(launch_matvec(c, PRO_NORM, EPI_SWIGLU, s));
+        } else if (k == 4) {
+            MvLaunch d; d.w = y.w2; d.xq = aqf; d.x = u; d.y = x; d.sp = sp; d.n_tokens = 1;
+            if (cu) CK(launch_matvec_cu(d, PRO_ACTF, EPI_RESID, s)); else CK(launch_matvec(d, PRO_ACTQ, EPI_RESID, s));
+        } else {
+            MvLaunch o; o.w = lm; o.x = x; o.g = g; o.sp = sp; o.y = logits; o.n_tokens = 1;
+            CK(mv(o, PRO_NORM, EPI_STORE));
+        }
+    };
+    const char * names[6] = {"qkv", "attn", "wo", "w13", "w2", "lm_head"};
+    const double bytes[6] = {3.0 * E * E / 32 * 20, 0, 1.0 * E * E / 32 * 20, 2.0 * F * E / 32 * 20, 1.0 * F * E / 32 * 20, 1.0 * V * E / 32 * 20};
+    // x is re-normalised by every RESID add; keep it bounded by re-filling before each graph (not timed)
+    hipGraph_t gr; hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    for (int l = 0; l < L; l++) for (int k = 0; k < 5; k++) op(k, l);
+    op(5, 0);
+    CK(hipStreamEndCapture(s, &gr));
+    CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; i++) CK(hipGraphLaunch(ge, s));
+    CK(hipStreamSynchronize(s));
+    const int R = 20;
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < R; i++) CK(hipGraphLaunch(ge, s));
+    CK(hipEventRecord(e1, s)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("n_past %d  token %.3f ms  (%.0f tok/s)\n", n_past, ms / R, 1e3 * R / ms);
+    // per kind: one graph per kind with its 32 (or 8) launches back to back
+    for (int k = 0; k < 6; k++) {
+        hipGraph_t g2; hipGraphExec_t ge2;
+        int n = k < 5 ? L : 8;
+        CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+        for (int l = 0; l < n; l++) op(k, l);
+        CK(hipStreamEndCapture(s, &g2));
+        CK(hipGraphInstantiate(&ge2, g2, nullptr, nullptr, 0));
+        CK(hipGraphLaunch(ge2, s)); CK(hipStreamSynchronize(s));
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < 5; i++) CK(hipGraphLaunch(ge2, s));
+        CK(hipEventRecord(e1, s)); CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        double us = ms * 1e3 / (5 * n);
+        printf("  %-8s %7.2f us/launch  %6.2f TB/s\n", names[k], us, bytes[k] ? bytes[k] / (us * 1e-6) / 1e12 : 0.0);
+        CK(hipGraphExecDestroy(ge2)); CK(hipGraphDestroy(g2));
+    }
+#ifdef LVK_PROBE_TIMING
+    {
+        const int kind = getenv("LVK_TRACE_KIND") ? atoi(getenv("LVK_TRACE_KIND")) : 5;
+        void * tr = lvk_probe_trace();
+        const size_t n = 256 * 16 * 64;
+        std::vector<unsigned long long> h(n);
+        // warm the same launch, then trace the 5th layer's instance
+        for (int l = 0; l < 4; l++) op(kind, l);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemset(tr, 0, n * 8));
+        op(kind, 4);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(h.data(), tr, n * 8, hipMemcpyDeviceToHost));
+        double sum_pro = 0, sum_end = 0, sum_issue = 0; int nw = 0;
+        double pe[4] = {0, 0, 0, 0}; int npw = 0;
+        std::vector<double> cs(60, 0), cw(60, 0); std::vector<int> cn(60, 0);
+        double maxend = 0;
+        for (int w = 0; w < 256 * 16; w++) {
+            unsigned long long * e = &h[(size_t) w * 64];
+            if (e[60] && e[63]) { npw++; pe[0] += e[61] - e[0]; pe[1] += e[62] - e[0]; pe[2] += e[63] - e[0]; }
+            if (!e[0] || !e[3]) continue;
+            nw++;
+            sum_issue += e[1] - e[0]; sum_pro += e[2] - e[0]; sum_end += e[3] - e[0];
+            maxend = std::max(maxend, (double) (e[3] - e[0]));
+            unsigned long long prev = e[2];
+            for (int q = 4; q + 1 < 56 && e[q] && e[q + 1]; q += 2) {
+                int ci = (q - 4) / 2;
+                cs[ci] += e[q + 1] - e[q]; cw[ci] += e[q] - prev; cn[ci]++;
+                prev = e[q + 1];
+            }
+        }
+        printf("trace kind %s: %d compute waves; avg cycles from entry: staged-seen %.0f act-ready %.0f end %.0f (max end %.0f)\n",
+               names[kind], nw, sum_issue / nw, sum_pro / nw, sum_end / nw, maxend);
+        printf("  (loader waves %d) staged-issued %.0f  first-publish %.0f  end %.0f\n", npw, pe[0] / std::max(1, npw), pe[1] / std::max(1, npw), pe[2] / std::max(1, npw));
+        for (int c = 0; c < 26 && cn[c]; c++)
+            printf("  chunk %2d: n %5d  gap-before %6.0f  body %6.0f\n", c, cn[c], cw[c] / cn[c], cs[c] / cn[c]);
+    }
+#endif
+    return 0;
+}
