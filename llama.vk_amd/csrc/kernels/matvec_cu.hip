@@ -476,8 +476,12 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
             case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 4096>(P, s); break;
             case EPI_RESID: if (pro == PRO_ACTQ) return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096>(P, s); break;
         }
+        // operator API (lvk_mul_mat_q: plain quantize of an f32 input)
+        if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 4096>(P, s);
     } else if (K == 11008) {
         if (epi == EPI_RESID && pro == PRO_ACTF) return go<4, 0, 4, PRO_ACTF, EPI_RESID, 11008>(P, s);
+        if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 0, 4, PRO_ACTF, EPI_STORE, 11008>(P, s);
+        if (epi == EPI_STORE && pro == PRO_NORM) return go<4, 0, 4, PRO_NORM, EPI_STORE, 11008>(P, s);
     }
     return hipErrorNotSupported;
 }

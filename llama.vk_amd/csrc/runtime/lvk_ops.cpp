@@ -96,7 +96,12 @@ static int mul_mat_impl(int type, const void * w, int m, int k, const float * g,
     lvk::MvLaunch L;
     L.w = q; L.sp = spd; L.n_tokens = n; L.y = yd;
     float * xd = dv.up(x, (size_t) n * k);
-    if (norm) {
+    if (n == 1 && lvk::matvec_cu_supported(k)) {
+        // single column: the decode kernel (matvec_cu.hip), quantizing in its prologue
+        L.x = xd;
+        if (norm) L.g = dv.up(g, (size_t) k);
+        LVK_HIP(lvk::launch_matvec_cu(L, norm ? lvk::PRO_NORM : lvk::PRO_ACTF, lvk::EPI_STORE, nullptr));
+    } else if (norm) {
         L.x = xd;
         L.g = dv.up(g, (size_t) k);
         LVK_HIP(lvk::launch_matvec(L, lvk::PRO_NORM, lvk::EPI_STORE, nullptr));

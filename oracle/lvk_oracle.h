@@ -5,7 +5,7 @@
  * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it; the
  * product (llama.vk_amd/) never does.
  *
- * Pinning: tests/test_oracle_vs_ref.py checks every function below bit-for-bit
+ * Pinning: tests/test_oracle_golden.py checks the functions below bit-for-bit
  * against the reference build (oracle/_ref/libref.so) and the committed golden
  * vectors in tests/golden/.
  */
