@@ -321,3 +321,20 @@ const char * llama_print_system_info(void) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// include/ggml.h: the ggml calls of the reference example programs
+// ---------------------------------------------------------------------------
+#include "../../../include/ggml.h"
+
+struct ggml_context { int unused; };
+
+static int64_t g_t0_us = 0;
+void ggml_time_init(void) { g_t0_us = lvk::now_us(); }
+int64_t ggml_time_ms(void) { return (lvk::now_us() - g_t0_us) / 1000; }
+int64_t ggml_time_us(void) { return lvk::now_us() - g_t0_us; }
+struct ggml_context * ggml_init(struct ggml_init_params params) {
+    (void) params;
+    return new ggml_context{0};
+}
+void ggml_free(struct ggml_context * ctx) { delete ctx; }

@@ -1,0 +1,63 @@
+"""The reference's own example programs, unmodified, linked to this library.
+
+tools/dropin/Makefile compiles /root/reference/examples/{main,perplexity,
+embedding,quantize} against include/llama.h (+ include/ggml.h) and links them
+to libllama_vk_amd.so instead of the reference's llama.o/ggml.o -- the drop-in
+boundary of INTEGRATION.md.  The reference CPU build of the same main
+(oracle/_ref/main) is the checker: with greedy sampling, bit-exact logits give
+the identical generated text.
+"""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DROPIN = os.path.join(ROOT, "tools", "dropin", "bin")
+REF_MAIN = os.path.join(ROOT, "oracle", "_ref", "main")
+
+
+def _need(path):
+    if not os.path.exists(path):
+        pytest.skip("%s not built (make -C tools/dropin / oracle needs /root/reference)" % path)
+
+
+def _run(args, timeout=300):
+    p = subprocess.run(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=timeout)
+    assert p.returncode == 0, p.stderr.decode(errors="replace")[-2000:]
+    return p.stdout, p.stderr
+
+
+def test_dropin_quantize_matches_library_tool(tmp_path):
+    """examples/quantize (reference source) on this library: f32 -> q4_0/q4_1 bytes
+    equal llama_model_quantize called directly (pinned against the reference in
+    test_abi.py)."""
+    exe = os.path.join(DROPIN, "quantize")
+    _need(exe)
+    import numpy as np
+    import lvk
+    from test_abi import _f32_model
+    src = str(tmp_path / "f32.bin")
+    _f32_model(src, np.random.default_rng(5))
+    for itype in (2, 3):
+        a = str(tmp_path / ("a%d.bin" % itype))
+        b = str(tmp_path / ("b%d.bin" % itype))
+        _run([exe, src, a, str(itype)])
+        assert lvk.lib.llama_model_quantize(src.encode(), b.encode(), itype) == 0
+        assert open(a, "rb").read() == open(b, "rb").read()
+
+
+@pytest.mark.gpu
+def test_dropin_main_greedy_text_matches_reference_cpu(tiny_models):
+    """examples/main on the GPU library vs the reference AVX2 build on the CPU:
+    same model, prompt, seed and greedy sampling -> the same text."""
+    exe = os.path.join(DROPIN, "main")
+    _need(exe)
+    _need(REF_MAIN)
+    args = ["-m", tiny_models["tiny_q4_0"], "-p", "Building a website can be done in 10 simple steps:",
+            "-n", "48", "--temp", "0", "-s", "1", "-c", "256", "--ignore-eos"]
+    gpu_out, gpu_err = _run([exe] + args + ["-t", "1"])
+    cpu_out, _ = _run([REF_MAIN] + args + ["-t", "8"])
+    assert gpu_out == cpu_out
+    assert len(gpu_out) > 60
+    assert b"llama_print_timings" in gpu_err
