@@ -18,6 +18,7 @@
 // the reduce is a fixed DPP pattern.
 #include "lvk_device.h"
 #include "lvk_kernels.h"
+#include "matvec_common.h"
 
 namespace lvk {
 
@@ -201,6 +202,21 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
             }
         }
     }
+    if constexpr (QT == Q4_1) {
+        // quantize_row_q4_1 (ggml.c:847-920) of the HD/64 blocks staged in ob
+        if (tid < HD / 16) {
+            const int bb = tid >> 2, k = tid & 3;
+            const int blk = (h * HD + half * (HD / 2)) / 32 + bb;
+            float dd, mm;
+            uint32_t qw;
+            mv::q41_block_lds(ob + bb * 32, k, dd, mm, qw);
+            ((uint32_t *) (out.qs + (size_t) t * out.nb + blk))[k] = qw;
+            if (k == 0) {
+                out.d[(size_t) t * out.nb + blk] = dd;
+                out.m[(size_t) t * out.nb + blk] = mm;
+            }
+        }
+    }
 }
 
 }  // namespace
@@ -208,12 +224,16 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s) {
     const int hd = A.n_embd / A.n_head;
     if (hd != 128 || A.n_ctx % 32 || A.n_ctx < 128) return hipErrorInvalidValue;
-    if (A.out_qtype != Q4_0) return hipErrorNotSupported;
+    if (A.out_qtype != Q4_0 && A.out_qtype != Q4_1) return hipErrorNotSupported;
     const float scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
     dim3 grid(A.n_head, A.n_tokens, 2);
     const size_t lds = (size_t) A.n_ctx * 6 + 64;
-    LVK_LAUNCH((k_attn<128, Q4_0>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,
-                       A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out);
+    if (A.out_qtype == Q4_1)
+        LVK_LAUNCH((k_attn<128, Q4_1>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,
+                   A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out);
+    else
+        LVK_LAUNCH((k_attn<128, Q4_0>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,
+                   A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out);
     return hipGetLastError();
 }
 

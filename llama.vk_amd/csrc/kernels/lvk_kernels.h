@@ -97,6 +97,8 @@ struct MvLaunch {
 };
 
 hipError_t launch_matvec(const MvLaunch & L, int pro, int epi, hipStream_t s);
+// the same for Q4_1 weights (matvec_q41.hip); launch_matvec forwards here
+hipError_t launch_matvec_q41(const MvLaunch & L, int pro, int epi, hipStream_t s);
 
 // single-token decode matvec, one workgroup per CU (matvec_cu.hip).  Row
 // lengths compiled in: matvec_cu_supported(K).  Returns hipErrorNotSupported
@@ -131,7 +133,9 @@ hipError_t launch_repack(const void * src_rows, int qtype, int M, int K, uint4 *
                          hipStream_t s, int interleave4 = 0);
 // bytes of the two image arrays for an M x K matrix
 inline size_t qimage_nib_bytes(int M, int K) { return (size_t) M * ((K / 32 + 31) / 32) * 512; }
-inline size_t qimage_scl_bytes(int M, int K) { return (size_t) M * ((K / 32 + 31) / 32) * 128; }
+inline size_t qimage_scl_bytes(int M, int K, int qtype = Q4_0) {
+    return (size_t) M * ((K / 32 + 31) / 32) * 128 * (qtype == Q4_1 ? 2 : 1);
+}
 
 // operator-level helpers used by the C ABI tests
 hipError_t launch_quantize_act(const float * x, int N, int K, int qtype, ActQ out, hipStream_t s);

@@ -64,5 +64,77 @@ __device__ __forceinline__ float octet_reduce(float a) {
     return c + __shfl_xor(c, 1);                // (r0+r2) + (r1+r3)
 }
 
+// AVX2 emulation helpers (ggml.c:890-915): cvtps_epi32 of an out-of-range value
+// gives INT_MIN; packs_epi32 + packs_epi16 saturate to int8; packNibbles packs
+// (b0 | b1 << 4) with unsigned saturation (ggml.c:440-452)
+__device__ __forceinline__ int32_t cvt_ps_epi32(float v) {
+    if (!(v >= -2147483648.0f && v < 2147483648.0f)) return (int32_t) 0x80000000u;
+    return (int32_t) v;
+}
+__device__ __forceinline__ uint32_t sat8u(int32_t v) {
+    v = v > 127 ? 127 : (v < -128 ? -128 : v);
+    return (uint32_t) (uint8_t) (int8_t) v;
+}
+__device__ __forceinline__ uint32_t pack_nib(uint32_t b0, uint32_t b1) {
+    const uint32_t v = b0 | (b1 << 4);
+    return v > 255u ? 255u : v;
+}
+
+// the AVX2 max/min tree of quantize_row_q4_1 (ggml.c:857-871) on a block whose
+// element e is e8[l] of "lane" k = e/8, l = e%8: max(a,b) = a > b ? a : b, so
+// the sign of a zero extremum follows the reference's lane order
+struct MinMax { float mx, mn; };
+__device__ __forceinline__ MinMax q41_tree(const float (&cm)[8], const float (&cn)[8]) {
+    float x4[4], n4[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        x4[l] = cm[4 + l] > cm[l] ? cm[4 + l] : cm[l];
+        n4[l] = cn[4 + l] < cn[l] ? cn[4 + l] : cn[l];
+    }
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+        x4[l] = x4[l] > x4[l + 2] ? x4[l] : x4[l + 2];
+        n4[l] = n4[l] < n4[l + 2] ? n4[l] : n4[l + 2];
+    }
+    return {x4[0] > x4[1] ? x4[0] : x4[1], n4[0] < n4[1] ? n4[0] : n4[1]};
+}
+
+// quantize 8 elements of a block given its min and 1/d: 4 qs bytes
+__device__ __forceinline__ uint32_t q41_pack8(const float v[8], float vmin, float id) {
+    uint32_t qword = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const float t0 = v[2 * p] - vmin, t1 = v[2 * p + 1] - vmin;     // sub, then mul (ggml.c:883-886)
+        const float w0 = t0 * id, w1 = t1 * id;
+        const uint32_t b0 = sat8u(cvt_ps_epi32(__builtin_rintf(w0)));
+        const uint32_t b1 = sat8u(cvt_ps_epi32(__builtin_rintf(w1)));
+        qword |= pack_nib(b0, b1) << (8 * p);
+    }
+    return qword;
+}
+
+
+// quantize_row_q4_1 of 32 values staged in LDS (xb[0..31]); lanes k < 4 of the
+// calling group return qs word k; every lane returns d and m
+__device__ __forceinline__ void q41_block_lds(const float * xb, int k, float & d, float & m, uint32_t & qword) {
+    float cm[8], cn[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        const float a0 = xb[l], a1 = xb[8 + l], a2 = xb[16 + l], a3 = xb[24 + l];
+        float x = a0 > a1 ? a0 : a1;  x = x > a2 ? x : a2;  x = x > a3 ? x : a3;
+        float n = a0 < a1 ? a0 : a1;  n = n < a2 ? n : a2;  n = n < a3 ? n : a3;
+        cm[l] = x; cn[l] = n;
+    }
+    const MinMax mm = q41_tree(cm, cn);
+    d = (mm.mx - mm.mn) / 15.0f;
+    const float id = d != 0.0f ? 1.0f / d : 0.0f;
+    m = mm.mn;
+    float v[8];
+    const int kk = k & 3;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = xb[8 * kk + e];
+    qword = q41_pack8(v, mm.mn, id);
+}
+
 }  // namespace mv
 }  // namespace lvk

@@ -428,6 +428,7 @@ hipError_t go(const Params & P, int ngroups, int ntok, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_matvec(const MvLaunch & L, int pro, int epi, hipStream_t s) {
+    if (L.w.qtype == Q4_1) return launch_matvec_q41(L, pro, epi, s);
     if (L.w.qtype != Q4_0) return hipErrorNotSupported;
     if (L.w.M % 8 || L.w.K % 256) return hipErrorInvalidValue;
     Params P{};

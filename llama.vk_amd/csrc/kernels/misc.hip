@@ -2,6 +2,7 @@
 // quad-sliced HBM image, and a standalone activation quantizer.
 #include "lvk_device.h"
 #include "lvk_kernels.h"
+#include "matvec_common.h"
 
 namespace lvk {
 thread_local LaunchEvents g_launch_events;
@@ -78,6 +79,74 @@ __global__ void k_repack_q40(const uint8_t * __restrict__ src, int M, int K, uin
     scl[((size_t) g * NC + c) * 64 + lane] = make_float4(d[0], d[1], d[2], d[3]);
 }
 
+// Q4_1 file rows (d, m, qs[16]) -> octet image (matvec_q41.hip):
+//   a(i,j) = qs_i[j] | qs_i[8+j] << 8    (elements 2j, 2j+1, 16+2j, 17+2j, unsigned)
+//   W(p,j) = a(2p,j) | a(2p+1,j) << 16
+//   scl[g][c][0][8r+j] = {d(32c+8m+j)}, scl[g][c][1][8r+j] = {m(32c+8m+j)}, m = 0..3
+__global__ void k_repack_q41(const uint8_t * __restrict__ src, int M, int K, uint4 * __restrict__ nib,
+                             float4 * __restrict__ scl, int il4) {
+    const int nb = K / 32, NC = (nb + 31) / 32;
+    const long idx = (long) blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long) M * NC * 8) return;
+    const int j = (int) (idx & 7);
+    const long rc = idx >> 3;
+    const int row = (int) (rc / NC), c = (int) (rc % NC);
+    const int g = row / 8, r = row % 8;
+    const int lane = 8 * r + j;
+    const int srow = il4 ? ((row & 7) < 4 ? (row >> 3) * 4 + (row & 7) : M / 2 + (row >> 3) * 4 + (row & 7) - 4) : row;
+    const uint8_t * rb = src + (size_t) srow * nb * 24;
+    auto grp = [&](int i) -> uint32_t {
+        if (i >= nb) return 0u;
+        const uint8_t * b = rb + (size_t) i * 24 + 8;
+        return (uint32_t) b[j] | ((uint32_t) b[8 + j] << 8);
+    };
+    for (int sb = 0; sb < 4; ++sb) {
+        uint32_t w[4];
+        for (int k = 0; k < 4; ++k) {
+            const int i = 32 * c + 8 * sb + 2 * k;
+            w[k] = (i < nb) ? (grp(i) | (grp(i + 1) << 16)) : 0u;
+        }
+        nib[(((size_t) g * NC + c) * 4 + sb) * 64 + lane] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    float d[4], m[4];
+    for (int q = 0; q < 4; ++q) {
+        const int i = 32 * c + 8 * q + j;
+        d[q] = (i < nb) ? *(const float *) (rb + (size_t) i * 24) : 0.0f;
+        m[q] = (i < nb) ? *(const float *) (rb + (size_t) i * 24 + 4) : 0.0f;
+    }
+    scl[(((size_t) g * NC + c) * 2) * 64 + lane] = make_float4(d[0], d[1], d[2], d[3]);
+    scl[(((size_t) g * NC + c) * 2 + 1) * 64 + lane] = make_float4(m[0], m[1], m[2], m[3]);
+}
+
+// standalone Q4_1 activation quantizer (quantize_row_q4_1 AVX2, ggml.c:847-920),
+// one thread per block; output split d / m / qs in the reference nibble layout
+__global__ void k_quantize_q41(const float * __restrict__ x, int N, int K, ActQ out) {
+    const int nb = K / 32;
+    const long idx = (long) blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long) N * nb) return;
+    const int t = (int) (idx / nb), b = (int) (idx % nb);
+    const float * xb = x + (size_t) t * K + (size_t) b * 32;
+    float cm[8], cn[8];
+    for (int l = 0; l < 8; ++l) {
+        const float a0 = xb[l], a1 = xb[8 + l], a2 = xb[16 + l], a3 = xb[24 + l];
+        float mx = a0 > a1 ? a0 : a1;  mx = mx > a2 ? mx : a2;  mx = mx > a3 ? mx : a3;
+        float mn = a0 < a1 ? a0 : a1;  mn = mn < a2 ? mn : a2;  mn = mn < a3 ? mn : a3;
+        cm[l] = mx; cn[l] = mn;
+    }
+    const mv::MinMax mm = mv::q41_tree(cm, cn);
+    const float d = (mm.mx - mm.mn) / 15.0f;
+    const float id = d != 0.0f ? 1.0f / d : 0.0f;
+    uint32_t w[4];
+    for (int k = 0; k < 4; ++k) {
+        float v[8];
+        for (int e = 0; e < 8; ++e) v[e] = xb[8 * k + e];
+        w[k] = mv::q41_pack8(v, mm.mn, id);
+    }
+    out.d[idx] = d;
+    out.m[idx] = mm.mn;
+    out.qs[idx] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // standalone activation quantizer (quantize_row_q4_0 AVX2, ggml.c:621-685)
 // one thread per block; output split d / qs in the reference nibble layout
 __global__ void k_quantize_q40(const float * __restrict__ x, int N, int K, ActQ out) {
@@ -120,6 +189,11 @@ hipError_t launch_repack(const void * src_rows, int qtype, int M, int K, uint4 *
                            (const uint8_t *) src_rows, M, K, nib, (float4 *) scl, interleave4);
         return hipGetLastError();
     }
+    if (qtype == Q4_1) {
+        hipLaunchKernelGGL(k_repack_q41, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s,
+                           (const uint8_t *) src_rows, M, K, nib, (float4 *) scl, interleave4);
+        return hipGetLastError();
+    }
     return hipErrorNotSupported;
 }
 
@@ -128,6 +202,10 @@ hipError_t launch_quantize_act(const float * x, int N, int K, int qtype, ActQ ou
     const long n = (long) N * (K / 32);
     if (qtype == Q4_0) {
         hipLaunchKernelGGL(k_quantize_q40, dim3((unsigned) ((n + 127) / 128)), dim3(128), 0, s, x, N, K, out);
+        return hipGetLastError();
+    }
+    if (qtype == Q4_1) {
+        hipLaunchKernelGGL(k_quantize_q41, dim3((unsigned) ((n + 127) / 128)), dim3(128), 0, s, x, N, K, out);
         return hipGetLastError();
     }
     return hipErrorNotSupported;

@@ -254,7 +254,7 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
         QMatrix q;
         q.qtype = m.qtype; q.M = M; q.K = K;
         const size_t nib = qimage_nib_bytes(M, K);
-        const size_t scl = qimage_scl_bytes(M, K);
+        const size_t scl = qimage_scl_bytes(M, K, m.qtype);
         q.nib = (const uint4 *) m.alloc(nib);
         q.scl = m.alloc(scl);
         m.weight_bytes += (size_t) M * (K / 32) * (m.qtype == Q4_0 ? 20 : 24);

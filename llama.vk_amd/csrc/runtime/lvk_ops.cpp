@@ -88,7 +88,7 @@ static int mul_mat_impl(int type, const void * w, int m, int k, const float * g,
     lvk::QMatrix q;
     q.qtype = type; q.M = m; q.K = k;
     q.nib = (const uint4 *) dv.get(lvk::qimage_nib_bytes(m, k));
-    q.scl = dv.get(lvk::qimage_scl_bytes(m, k));
+    q.scl = dv.get(lvk::qimage_scl_bytes(m, k, type));
     LVK_HIP(lvk::launch_repack(wd, type, m, k, (uint4 *) q.nib, (void *) q.scl, nullptr));
     lvk::StepParams sp{0, n, 0, 0};
     lvk::StepParams * spd = dv.up(&sp, 1);
@@ -96,7 +96,12 @@ static int mul_mat_impl(int type, const void * w, int m, int k, const float * g,
     lvk::MvLaunch L;
     L.w = q; L.sp = spd; L.n_tokens = n; L.y = yd;
     float * xd = dv.up(x, (size_t) n * k);
-    if (n == 1 && lvk::matvec_cu_supported(k)) {
+    if (type == lvk::Q4_1) {
+        // Q4_1 kernels quantize the f32 input in their prologue
+        L.x = xd;
+        if (norm) L.g = dv.up(g, (size_t) k);
+        LVK_HIP(lvk::launch_matvec(L, norm ? lvk::PRO_NORM : lvk::PRO_ACTF, lvk::EPI_STORE, nullptr));
+    } else if (n == 1 && lvk::matvec_cu_supported(k)) {
         // single column: the decode kernel (matvec_cu.hip), quantizing in its prologue
         L.x = xd;
         if (norm) L.g = dv.up(g, (size_t) k);

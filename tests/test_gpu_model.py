@@ -24,10 +24,10 @@ def lvk(gpu_available):
     return m
 
 
-@pytest.mark.parametrize("graph", [True, False])
-def test_tiny_q4_0_matches_reference_golden(lvk, tiny_models, graph):
-    g = np.load(os.path.join(GOLD, "tiny_q4_0.npz"), allow_pickle=False)
-    m = lvk.Llama(tiny_models["tiny_q4_0"], n_ctx=512)
+@pytest.mark.parametrize("name,graph", [("tiny_q4_0", True), ("tiny_q4_0", False), ("tiny_q4_1", True)])
+def test_tiny_matches_reference_golden(lvk, tiny_models, name, graph):
+    g = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+    m = lvk.Llama(tiny_models[name], n_ctx=512)
     m.set_graph(graph)
     n_past, off = 0, 0
     for step, n in enumerate(g["chunks"]):
@@ -111,6 +111,28 @@ def test_7b_shaped_decode_vs_oracle(lvk, oracle, model_dir):
     assert np.array_equal(bits(a), bits(b))
     n_past, tok = len(toks), int(np.argmax(a[-1]))
     for _ in range(12):
+        a = m.eval([tok], n_past)
+        b = om.eval([tok], n_past)
+        assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past
+        n_past += 1
+        tok = int(np.argmax(a[-1]))
+    m.close()
+    om.close()
+
+
+def test_13b_shaped_q4_1_decode_vs_oracle(lvk, oracle, model_dir):
+    """LLaMA-13B layer shapes in Q4_1 (n_embd 5120, n_ff 13824, 40 heads), 1 layer:
+    Q4_1 quantizer + dot + attention output quantization on the GPU, bit-exact."""
+    from oracle_lib import gen_model
+    path = gen_model(os.path.join(model_dir, "w5120_l1_q41.bin"), n_embd=5120, n_head=40, n_layer=1, ftype=3, seed=11)
+    m = lvk.Llama(path, n_ctx=256)
+    om = oracle.model(path, 256)
+    toks = np.array([1, 450, 4996, 17354, 1701, 29916], np.int32)
+    a = m.eval(toks, 0)
+    b = om.eval(toks, 0)
+    assert np.array_equal(bits(a), bits(b))
+    n_past, tok = len(toks), int(np.argmax(a[-1]))
+    for _ in range(6):
         a = m.eval([tok], n_past)
         b = om.eval([tok], n_past)
         assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past

@@ -21,14 +21,17 @@ def lvk(gpu_available):
 
 
 @pytest.mark.parametrize("k", [256, 4096, 11008])
-def test_quantize_rows_q4_0(lvk, oracle, k):
+@pytest.mark.parametrize("qt", [2, 3])
+def test_quantize_rows(lvk, oracle, k, qt):
     rng = np.random.default_rng(k)
     x = np.concatenate([rng.standard_normal((4, k)) * s for s in (1e-3, 1.0, 50.0)]).astype(np.float32)
     x[0, :32] = 0.0          # an all-zero block (id = 0 branch)
     x[1, 5] = 1e-30          # tiny values
-    got = lvk.quantize_rows(x, 2)
+    x[2, 64:96] = -0.0       # a block of negative zeros (max/min tree order)
+    x[3, 96:128] = 7.25      # a constant block (d = 0 for Q4_1)
+    got = lvk.quantize_rows(x, qt)
     for i, row in enumerate(x):
-        assert np.array_equal(got[i], oracle.quantize(row, 2)), "row %d" % i
+        assert np.array_equal(got[i], oracle.quantize(row, qt)), "row %d" % i
 
 
 def _weights(oracle, rng, m, k, qt, scale=0.02):
@@ -47,6 +50,31 @@ def test_mul_mat_q4_0(lvk, oracle, m, k, n):
     x = (rng.standard_normal((n, k)) * 1.3).astype(np.float32)
     got = lvk.mul_mat_q(2, wq, m, k, x)
     want = _oracle_mm(oracle, wq, [oracle.quantize(r, 2) for r in x], k, 2)
+    assert np.array_equal(bits(got), bits(want))
+
+
+@pytest.mark.parametrize("m,k,n", [(64, 256, 1), (32, 5120, 1), (16, 13824, 1), (48, 5120, 3), (16, 1024, 8)])
+def test_mul_mat_q4_1(lvk, oracle, m, k, n):
+    rng = np.random.default_rng(m * 5 + k + n)
+    wq = _weights(oracle, rng, m, k, 3)
+    x = (rng.standard_normal((n, k)) * 0.9).astype(np.float32)
+    x[0, :32] = 0.25                                        # constant block: d = 0
+    got = lvk.mul_mat_q(3, wq, m, k, x)
+    want = _oracle_mm(oracle, wq, [oracle.quantize(r, 3) for r in x], k, 3)
+    assert np.array_equal(bits(got), bits(want))
+
+
+@pytest.mark.parametrize("m,k,n", [(64, 256, 1), (32, 5120, 1), (32, 5120, 5)])
+def test_mul_mat_q4_1_rmsnorm_prologue(lvk, oracle, m, k, n):
+    rng = np.random.default_rng(m + k * 7 + n)
+    wq = _weights(oracle, rng, m, k, 3)
+    x = (rng.standard_normal((n, k)) * 2.0).astype(np.float32)
+    g = (1.0 + 0.1 * rng.standard_normal(k)).astype(np.float32)
+    got = lvk.mul_mat_q_norm(3, wq, m, k, g, x)
+    xn = np.zeros_like(x)
+    oracle.lib.orc_rms_norm(x, k, n, xn)
+    xn = (g[None, :] * xn).astype(np.float32)
+    want = _oracle_mm(oracle, wq, [oracle.quantize(r, 3) for r in xn], k, 3)
     assert np.array_equal(bits(got), bits(want))
 
 
