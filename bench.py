@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 MODEL_BYTES_7B = 4130490880    # algorithmic weight bytes per token
+MODEL_BYTES_13B_Q41 = 9640369920   # 13B Q4_1 weight bytes per token
 REF_PUBLISHED_TOKS = 16.3      # 7B Q4_0 predict 61.41 ms/token
 
 
@@ -113,6 +114,8 @@ def main():
     ap.add_argument("--prompt-evals", type=int, default=3)
     ap.add_argument("--profile-steps", type=int, default=48)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-13b", action="store_true", help="skip the 13B Q4_1 decode line (BASELINE configs[3])")
+    ap.add_argument("--steps-13b", type=int, default=96)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
     args = ap.parse_args()
@@ -196,9 +199,36 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": bpl,
                 "avg_launch_us": avg_s * 1e6}
     step_gbs = value / n_gpus * MODEL_BYTES_7B / 1e9
+
+    # 13B Q4_1 single-stream decode (BASELINE.json configs[3]), same loop
+    q41 = None
+    if not args.no_13b:
+        m.close()
+        path13 = os.path.join(os.path.dirname(args.model), "llama-13b-q4_1.bin")
+        ensure_model(path13, rank, pg, dict(n_embd=5120, n_head=40, n_layer=40, ftype=3, seed=2))
+        m13 = lvk.Llama(path13, n_ctx=n_ctx)
+        lg = m13.eval(ptoks, 0)
+        tok = int(np.argmax(lg[-1]))
+        for i in range(4):
+            lg = m13.eval([tok], 16 + i)
+            tok = int(np.argmax(lg[-1]))
+        barrier(pg)
+        t0 = time.perf_counter()
+        for i in range(args.steps_13b):
+            lg = m13.eval([tok], 16 + (i % (n_ctx - 16)))
+            tok = int(np.argmax(lg[-1]))
+        t13 = all_max(pg, time.perf_counter() - t0)
+        m13.close()
+        r13 = args.steps_13b / t13
+        q41 = {"value": n_gpus * r13, "unit": "tok/s", "steps": args.steps_13b,
+               "workload": "LLaMA-13B Q4_1 (synthetic, seed 2) single-stream greedy decode, positions 16.., n_ctx 512",
+               "model_bytes_per_token": MODEL_BYTES_13B_Q41,
+               "frac_hbm_roofline": r13 * MODEL_BYTES_13B_Q41 / 1e9 / HBM_PEAK_GBS,
+               "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_13B_Q41}
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        m.close()
+        if args.no_13b:
+            m.close()
         cpu = cpu_baseline(args.model, args.cpu_budget)
 
     if rank == 0:
@@ -216,6 +246,7 @@ def main():
             "step_roofline": {"model_bytes_per_token": MODEL_BYTES_7B, "achieved_gbs": step_gbs,
                               "frac": step_gbs / HBM_PEAK_GBS, "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_7B},
             "prompt_eval": prompt,
+            "decode_13b_q4_1": q41,
             "kernels": kernels,
             "cpu_baseline": cpu,
             "load_s": load_s,
