@@ -105,6 +105,47 @@ def cpu_baseline(path, budget_s=15.0):
             "prompt_tok_s": 16 / t_prompt}
 
 
+def layer_split_decode(args, m_full, rank, ws, local, pg, n_ctx, ptoks):
+    """greedy decode through a ws-stage layer split of the 7B file (one stage per
+    rank, residual stream over RCCL send/recv); returns the rank-0 report"""
+    import datetime
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import lvk
+    from pipeline import StagePipeline, layer_ranges
+    torch.cuda.set_device(local)
+    grp = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=120))
+    hp = lvk.model_hparams(args.model)
+    lr = layer_ranges(hp["n_layer"], ws)[rank]
+    st = lvk.Llama(args.model, n_ctx=n_ctx, layers=lr)
+    pipe = StagePipeline(st, hp["n_embd"], n_ctx, dist, on_device=True, device="cuda:%d" % local, group=grp)
+    lg = pipe.eval(list(ptoks), 0)
+    tok = pipe.greedy_next(lg)
+    n_past = len(ptoks)
+    for _ in range(4):
+        lg = pipe.eval([tok], n_past)
+        tok = pipe.greedy_next(lg)
+        n_past += 1
+    dist.barrier(group=grp)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps_split):
+        lg = pipe.eval([tok], n_past)
+        tok = pipe.greedy_next(lg)
+        n_past = n_past + 1 if n_past + 1 < n_ctx else len(ptoks)
+    torch.cuda.synchronize()
+    dist.barrier(group=grp)
+    dt = all_max(pg, time.perf_counter() - t0)
+    st.close()
+    return {"value": args.steps_split / dt, "unit": "tok/s", "stages": ws, "steps": args.steps_split,
+            "layers_per_stage": [list(x) for x in layer_ranges(hp["n_layer"], ws)],
+            "workload": "LLaMA-7B Q4_0 greedy decode, layers split over %d GPUs (one stage per GPU), "
+                        "residual stream f32 [4096] per token over RCCL send/recv; the 65B split is "
+                        "bench.py --split-only with a 65B file" % ws,
+            "ms_per_token": dt / args.steps_split * 1e3}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None)
@@ -116,6 +157,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-13b", action="store_true", help="skip the 13B Q4_1 decode line (BASELINE configs[3])")
     ap.add_argument("--steps-13b", type=int, default=96)
+    ap.add_argument("--no-split", action="store_true", help="N>1: skip the layer-split pipeline line (SURVEY 8e)")
+    ap.add_argument("--steps-split", type=int, default=64)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
     args = ap.parse_args()
@@ -200,6 +243,12 @@ def main():
                 "avg_launch_us": avg_s * 1e6}
     step_gbs = value / n_gpus * MODEL_BYTES_7B / 1e9
 
+    # N > 1: the same 7B model split by layers over the ranks (SURVEY.md 8e
+    # pipeline: RCCL send/recv of the residual stream between stages)
+    split = None
+    if ws > 1 and not args.no_split:
+        split = layer_split_decode(args, m, rank, ws, local, pg, n_ctx, ptoks)
+
     # 13B Q4_1 single-stream decode (BASELINE.json configs[3]), same loop
     q41 = None
     if not args.no_13b:
@@ -247,6 +296,7 @@ def main():
                               "frac": step_gbs / HBM_PEAK_GBS, "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_7B},
             "prompt_eval": prompt,
             "decode_13b_q4_1": q41,
+            "layer_split": split,
             "kernels": kernels,
             "cpu_baseline": cpu,
             "load_s": load_s,

@@ -70,6 +70,26 @@ LVK_API size_t lvk_weight_bytes(struct llama_context * ctx);
 /* 1 = replay the captured decode graph for single-token evals (default), 0 = eager */
 LVK_API void lvk_set_graph(struct llama_context * ctx, int on);
 
+/* Pipeline stages (the 65B layer split).  A stage context holds
+ * layers [layer_begin, layer_end) of the model file (weights and KV cache); the
+ * first stage (layer_begin == 0) also holds the token embeddings, the last one
+ * (layer_end == n_layer) the final norm and lm_head.  This replaces running
+ * llama_eval_internal (llama.cpp:927-1197) as one process: the residual stream
+ * `inpL` is handed from stage s to s+1 (RCCL send/recv in
+ * llama.vk_amd/pipeline.py).  NULL on error. */
+LVK_API struct llama_context * lvk_init_stage(const char * path_model, struct llama_context_params params,
+                                              int layer_begin, int layer_end);
+/* run the stage on n_tokens at positions n_past..: the first stage embeds tokens,
+ * the others start from the residual stream set by lvk_stage_set_x; the last
+ * stage leaves logits for llama_get_logits.  0 on success, 1 on error. */
+LVK_API int lvk_stage_eval(struct llama_context * ctx, const int * tokens, int n_tokens, int n_past);
+/* copy the residual stream x [n_tokens][n_embd] f32 out of / into the stage;
+ * buf is memory of the context's HIP device when on_device != 0, else host */
+LVK_API int lvk_stage_get_x(struct llama_context * ctx, void * buf, int n_tokens, int on_device);
+LVK_API int lvk_stage_set_x(struct llama_context * ctx, const void * buf, int n_tokens, int on_device);
+/* the stage's layer range; returns the model's n_layer */
+LVK_API int lvk_stage_layers(struct llama_context * ctx, int * layer_begin, int * layer_end);
+
 #ifdef __cplusplus
 }
 #endif

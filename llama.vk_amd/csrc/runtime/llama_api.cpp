@@ -14,6 +14,7 @@
 #include <sys/mman.h>
 
 #include "../../../include/llama.h"
+#include "../../../include/lvk_ops.h"
 #include "lvk_context.h"
 
 namespace {
@@ -175,7 +176,8 @@ struct llama_context_params llama_context_default_params(void) {
 bool llama_mmap_supported(void) { return true; }
 bool llama_mlock_supported(void) { return true; }
 
-struct llama_context * llama_init_from_file(const char * path_model, struct llama_context_params params) {
+static llama_context * init_context(const char * path_model, struct llama_context_params params, int layer_begin,
+                                    int layer_end) {
     llama_context * ctx = new llama_context;
     lvk::Context & c = ctx->c;
     c.t_start_us = lvk::now_us();
@@ -192,7 +194,7 @@ struct llama_context * llama_init_from_file(const char * path_model, struct llam
         hipStream_t ls = nullptr;
         if (!params.vocab_only) LVK_HIP(hipStreamCreateWithFlags(&ls, hipStreamNonBlocking));
         lvk::load_model(c.model, path_model, params.vocab_only, ls, params.progress_callback,
-                        params.progress_callback_user_data);
+                        params.progress_callback_user_data, layer_begin, layer_end);
         if (ls) (void) hipStreamDestroy(ls);
         c.model.hp.n_ctx = (uint32_t) params.n_ctx;
         if (!params.vocab_only) {
@@ -207,6 +209,50 @@ struct llama_context * llama_init_from_file(const char * path_model, struct llam
     }
     c.t_load_us = lvk::now_us() - c.t_start_us;
     return ctx;
+}
+
+struct llama_context * llama_init_from_file(const char * path_model, struct llama_context_params params) {
+    return init_context(path_model, params, 0, -1);
+}
+
+// ---------------------------------------------------------------------------
+// pipeline stages (include/lvk_ops.h)
+// ---------------------------------------------------------------------------
+struct llama_context * lvk_init_stage(const char * path_model, struct llama_context_params params, int layer_begin,
+                                      int layer_end) {
+    if (params.vocab_only || layer_begin < 0 || layer_end <= layer_begin) {
+        fprintf(stderr, "%s: bad layer range [%d, %d)\n", __func__, layer_begin, layer_end);
+        return nullptr;
+    }
+    return init_context(path_model, params, layer_begin, layer_end);
+}
+
+int lvk_stage_eval(struct llama_context * ctx, const llama_token * tokens, int n_tokens, int n_past) {
+    try {
+        ctx->c.eval(tokens, n_tokens, n_past);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());
+        return 1;
+    }
+    return 0;
+}
+
+int lvk_stage_get_x(struct llama_context * ctx, void * buf, int n_tokens, int on_device) {
+    try { ctx->c.x_copy(buf, n_tokens, false, on_device != 0); }
+    catch (const lvk::Error & e) { fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str()); return 1; }
+    return 0;
+}
+
+int lvk_stage_set_x(struct llama_context * ctx, const void * buf, int n_tokens, int on_device) {
+    try { ctx->c.x_copy(const_cast<void *>(buf), n_tokens, true, on_device != 0); }
+    catch (const lvk::Error & e) { fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str()); return 1; }
+    return 0;
+}
+
+int lvk_stage_layers(struct llama_context * ctx, int * layer_begin, int * layer_end) {
+    *layer_begin = ctx->c.model.layer_begin;
+    *layer_end = ctx->c.model.layer_end;
+    return (int) ctx->c.model.hp.n_layer;
 }
 
 void llama_free(struct llama_context * ctx) { delete ctx; }

@@ -57,7 +57,7 @@ void Context::init(const llama_context_params & p) {
     logits_all = p.logits_all;
     want_embedding = p.embedding;
     const HParams & hp = model.hp;
-    const size_t E = hp.n_embd, L = hp.n_layer, V = hp.n_vocab, H = hp.n_head, F = hp.n_ff();
+    const size_t E = hp.n_embd, L = model.layers.size(), V = hp.n_vocab, H = hp.n_head, F = hp.n_ff();
     const size_t hd = E / H, C = (size_t) n_ctx;
     if (n_ctx < 64 || n_ctx % 32) throw Error("llama.vk_amd: n_ctx must be a multiple of 32 and >= 64");
     kc = (uint16_t *) model.alloc(L * C * E * 2);
@@ -156,7 +156,8 @@ void Context::enqueue_forward(int n, bool last_only) {
     const size_t CE = (size_t) n_ctx * E;
     // single-token FFN: W1|W3 hands silu(w1 x)*(w3 x) to W2 in f32, W2 quantizes it
     const bool ffn_f32 = n == 1 && model.qtype == Q4_0 && matvec_cu_supported(E) && matvec_cu_supported(F);
-    timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_d, n, x, stream); });
+    if (model.has_embed)
+        timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_d, n, x, stream); });
     for (size_t il = 0; il < model.layers.size(); ++il) {
         const Layer & ly = model.layers[il];
         MvLaunch a;
@@ -182,12 +183,13 @@ void Context::enqueue_forward(int n, bool last_only) {
             timed_launch(K_W2, qbytes(ly.w2), [&] { return launch_matvec(d, PRO_ACTQ, EPI_RESID, stream); });
         }
     }
+    if (!model.has_head) return;   // not the last pipeline stage: x is the output
     MvLaunch o;
     o.w = model.output; o.x = x; o.g = model.norm; o.sp = sp_d; o.y = logits_d;
     o.tok0 = last_only ? n - 1 : 0;
     o.n_tokens = last_only ? 1 : n;
     timed_launch(K_LMHEAD, qbytes(model.output), [&] { return mv_launch(o, PRO_NORM, EPI_STORE, stream); });
-    if (want_embedding)
+    if (want_embedding && model.has_head)
         LVK_HIP(launch_rmsnorm_rows(x + (size_t) (n - 1) * E, model.norm, E, 1, emb_d, stream));
 }
 
@@ -208,11 +210,14 @@ void Context::eval(const int * tokens, int n, int n_past) {
     const HParams & hp = model.hp;
     const int V = (int) hp.n_vocab;
     if (n <= 0 || n_past < 0 || n_past + n > n_ctx) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
-    for (int i = 0; i < n; ++i)
-        if (tokens[i] < 0 || tokens[i] >= V) throw Error("llama.vk_amd: token id out of range");
+    if (model.has_embed) {
+        if (!tokens) throw Error("llama.vk_amd: the first stage needs tokens");
+        for (int i = 0; i < n; ++i)
+            if (tokens[i] < 0 || tokens[i] >= V) throw Error("llama.vk_amd: token id out of range");
+        std::memcpy(tok_h, tokens, sizeof(int) * (size_t) n);
+    }
     sp_h->n_past = n_past;
     sp_h->n_tokens = n;
-    std::memcpy(tok_h, tokens, sizeof(int) * (size_t) n);
     LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
     LVK_HIP(hipMemcpyAsync(tok_d, tok_h, sizeof(int) * (size_t) n, hipMemcpyHostToDevice, stream));
     const bool last_only = !logits_all;
@@ -223,9 +228,11 @@ void Context::eval(const int * tokens, int n, int n_past) {
         enqueue_forward(n, last_only);
     }
     const int rows = last_only ? 1 : n;
-    logits.resize((size_t) rows * V);
-    LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost, stream));
-    if (want_embedding) {
+    if (model.has_head) {
+        logits.resize((size_t) rows * V);
+        LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost, stream));
+    }
+    if (want_embedding && model.has_head) {
         embedding.resize(hp.n_embd);
         LVK_HIP(hipMemcpyAsync(embedding.data(), emb_d, sizeof(float) * hp.n_embd, hipMemcpyDeviceToHost, stream));
     }
@@ -234,7 +241,7 @@ void Context::eval(const int * tokens, int n, int n_past) {
 }
 
 size_t Context::kv_bytes() const {
-    return 2u * (size_t) model.hp.n_layer * n_ctx * model.hp.n_embd * 2u;
+    return 2u * (size_t) model.layers.size() * n_ctx * model.hp.n_embd * 2u;
 }
 
 void Context::kv_get() {
@@ -251,4 +258,17 @@ void Context::kv_set(const uint8_t * src, size_t n) {
     LVK_HIP(hipMemcpy(vc, src + half, half, hipMemcpyHostToDevice));
 }
 
+}  // namespace lvk
+
+namespace lvk {
+// pipeline stages: the residual stream crosses stage boundaries
+void Context::x_copy(void * buf, int n, bool to_ctx, bool on_device) {
+    if (n <= 0 || n > n_ctx) throw Error("llama.vk_amd: bad token count for the stage residual stream");
+    const size_t bytes = sizeof(float) * (size_t) n * model.hp.n_embd;
+    const hipMemcpyKind k = to_ctx ? (on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice)
+                                   : (on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost);
+    if (to_ctx) LVK_HIP(hipMemcpyAsync(x, buf, bytes, k, stream));
+    else LVK_HIP(hipMemcpyAsync(buf, x, bytes, k, stream));
+    LVK_HIP(hipStreamSynchronize(stream));
+}
 }  // namespace lvk

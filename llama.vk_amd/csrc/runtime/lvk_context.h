@@ -73,6 +73,8 @@ struct Context {
     ~Context();
     void init(const llama_context_params & p);
     void eval(const int * tokens, int n, int n_past);
+    // stage boundary: copy the residual stream x [n][E] to (to_ctx) or from the context
+    void x_copy(void * buf, int n, bool to_ctx, bool on_device);
     void enqueue_forward(int n, bool last_only);
     void build_graph();
     void kv_get();

@@ -161,7 +161,7 @@ Model::~Model() {
 }
 
 void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_t s,
-                void (*progress)(float, void *), void * progress_ud) {
+                void (*progress)(float, void *), void * progress_ud, int layer_begin, int layer_end) {
     const auto t_start = std::chrono::steady_clock::now();
     std::vector<std::unique_ptr<MappedFile>> files;
     files.emplace_back(new MappedFile(path));
@@ -243,8 +243,16 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
     LVK_HIP(hipMalloc(&stage, stage_n));
     struct StageFree { void * p; ~StageFree() { (void) hipFree(p); } } stage_guard{stage};
 
-    size_t total = t_tok.size + t_out.size, done = 0;
-    total += (size_t) L * (3 * E * rb_E + E * rb_E + 2 * (size_t) F * rb_E + E * rb_F);
+    if (layer_end < 0) layer_end = (int) L;
+    if (layer_begin < 0 || layer_begin >= layer_end || layer_end > (int) L)
+        throw Error("llama.vk_amd: bad layer range [" + std::to_string(layer_begin) + ", " + std::to_string(layer_end) + ")");
+    m.layer_begin = layer_begin;
+    m.layer_end = layer_end;
+    m.has_embed = layer_begin == 0;
+    m.has_head = layer_end == (int) L;
+    const uint32_t LB = (uint32_t) layer_begin, LN = (uint32_t) (layer_end - layer_begin);
+    size_t total = (m.has_embed ? t_tok.size : 0) + (m.has_head ? t_out.size : 0), done = 0;
+    total += (size_t) LN * (3 * E * rb_E + E * rb_E + 2 * (size_t) F * rb_E + E * rb_F);
     auto tick = [&](size_t n) {
         done += n;
         if (progress) progress((float) ((double) done / (double) total), progress_ud);
@@ -270,21 +278,25 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
 
     // embeddings stay in file layout (gathered by row, ggml.c:6868-6895)
     m.emb_type = (int) t_tok.type;
-    m.tok_emb = m.alloc(t_tok.size);
-    LVK_HIP(hipMemcpy(m.tok_emb, t_tok.host, t_tok.size, hipMemcpyHostToDevice));
-    tick(t_tok.size);
+    if (m.has_embed) {
+        m.tok_emb = m.alloc(t_tok.size);
+        LVK_HIP(hipMemcpy(m.tok_emb, t_tok.host, t_tok.size, hipMemcpyHostToDevice));
+        tick(t_tok.size);
+    }
     if (t_norm.type != 0) throw Error("norm.weight must be f32");
-    m.norm = (float *) m.alloc(4u * E);
-    LVK_HIP(hipMemcpy(m.norm, t_norm.host, 4u * E, hipMemcpyHostToDevice));
-    // lm_head
-    LVK_HIP(hipMemcpy(stage, t_out.host, t_out.size, hipMemcpyHostToDevice));
-    m.output = make_matrix((int) V, (int) E);
-    repack(m.output);
-    tick(t_out.size);
+    if (m.has_head) {
+        m.norm = (float *) m.alloc(4u * E);
+        LVK_HIP(hipMemcpy(m.norm, t_norm.host, 4u * E, hipMemcpyHostToDevice));
+        // lm_head
+        LVK_HIP(hipMemcpy(stage, t_out.host, t_out.size, hipMemcpyHostToDevice));
+        m.output = make_matrix((int) V, (int) E);
+        repack(m.output);
+        tick(t_out.size);
+    }
 
-    m.layers.resize(L);
-    for (uint32_t il = 0; il < L; ++il) {
-        Layer & ly = m.layers[il];
+    m.layers.resize(LN);
+    for (uint32_t il = LB; il < LB + LN; ++il) {
+        Layer & ly = m.layers[il - LB];
         const std::string p = "layers." + std::to_string(il) + ".";
         Tensor an = get(p + "attention_norm.weight", {E});
         Tensor fn = get(p + "ffn_norm.weight", {E});

@@ -59,7 +59,10 @@ struct Model {
     void * tok_emb = nullptr;      // device, file layout
     float * norm = nullptr;        // [E]
     QMatrix output;                // [V][E]
-    std::vector<Layer> layers;
+    std::vector<Layer> layers;     // layers [layer_begin, layer_end) of the file
+    int layer_begin = 0, layer_end = 0;
+    bool has_embed = true;         // first pipeline stage: token embeddings resident
+    bool has_head = true;          // last stage: final norm + lm_head resident
     std::vector<DevBuf> bufs;      // owned device memory
     size_t weight_bytes = 0;       // bytes of weights resident in HBM (quad-sliced images)
     size_t file_bytes = 0;
@@ -70,8 +73,11 @@ struct Model {
 };
 
 // Load a ggjt v1 (or ggmf/ggml vocab-only) file.  vocab_only stops after the
-// vocabulary.  Throws lvk::Error.
+// vocabulary.  layer_end < 0 means all layers; a partial range [layer_begin,
+// layer_end) is one pipeline stage: the embeddings are loaded
+// only when layer_begin == 0, the final norm + lm_head only when layer_end ==
+// n_layer.  Throws lvk::Error.
 void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_t s,
-                void (*progress)(float, void *), void * progress_ud);
+                void (*progress)(float, void *), void * progress_ud, int layer_begin = 0, int layer_end = -1);
 
 }  // namespace lvk

@@ -93,6 +93,11 @@ _sig("lvk_get_profile", C.c_int, [C.c_void_p, f64p, i64p, f64p, C.c_int])
 _sig("lvk_reset_profile", None, [C.c_void_p])
 _sig("lvk_weight_bytes", C.c_size_t, [C.c_void_p])
 _sig("lvk_set_graph", None, [C.c_void_p, C.c_int])
+_sig("lvk_init_stage", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, C.c_int])
+_sig("lvk_stage_eval", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
+_sig("lvk_stage_get_x", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
+_sig("lvk_stage_set_x", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
+_sig("lvk_stage_layers", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)])
 
 BLOCK_BYTES = {2: 20, 3: 24}
 KCLASS = ["embed", "qkv", "attention", "wo", "w13", "w2", "lm_head"]
@@ -106,7 +111,9 @@ def _check(rc, what):
 class Llama:
     """One llama_context (reference llama.h API, GPU forward pass)."""
 
-    def __init__(self, path, n_ctx=512, seed=1, logits_all=False, embedding=False, vocab_only=False, f16_kv=True):
+    def __init__(self, path, n_ctx=512, seed=1, logits_all=False, embedding=False, vocab_only=False, f16_kv=True,
+                 layers=None):
+        """layers=(begin, end): a pipeline stage holding only those layers (lvk_init_stage)"""
         p = lib.llama_context_default_params()
         p.n_ctx = n_ctx
         p.seed = seed
@@ -116,7 +123,10 @@ class Llama:
         p.vocab_only = vocab_only
         self._cb = PROGRESS_CB(lambda prog, ud: None)
         p.progress_callback = self._cb
-        self.ctx = lib.llama_init_from_file(path.encode(), p)
+        if layers is None:
+            self.ctx = lib.llama_init_from_file(path.encode(), p)
+        else:
+            self.ctx = lib.lvk_init_stage(path.encode(), p, int(layers[0]), int(layers[1]))
         if not self.ctx:
             raise RuntimeError("llama_init_from_file failed for %s" % path)
         self.logits_all = logits_all
@@ -130,6 +140,28 @@ class Llama:
         _check(lib.llama_eval(self.ctx, t, len(t), n_past, n_threads), "llama_eval")
         self._last_n = len(t)
         return self.logits()
+
+    # ---- pipeline stage (lvk_init_stage contexts)
+    def stage_eval(self, tokens, n_tokens, n_past):
+        """first stage: tokens (int32 array); later stages: tokens=None, input set by set_x"""
+        if tokens is None:
+            _check(lib.lvk_stage_eval(self.ctx, None, n_tokens, n_past), "lvk_stage_eval")
+        else:
+            t = np.ascontiguousarray(tokens, np.int32)
+            _check(lib.lvk_stage_eval(self.ctx, t.ctypes.data, len(t), n_past), "lvk_stage_eval")
+        self._last_n = n_tokens
+
+    def get_x(self, ptr, n_tokens, on_device):
+        """residual stream [n_tokens][n_embd] f32 -> ptr (device pointer if on_device)"""
+        _check(lib.lvk_stage_get_x(self.ctx, C.c_void_p(ptr), n_tokens, int(on_device)), "lvk_stage_get_x")
+
+    def set_x(self, ptr, n_tokens, on_device):
+        _check(lib.lvk_stage_set_x(self.ctx, C.c_void_p(ptr), n_tokens, int(on_device)), "lvk_stage_set_x")
+
+    def stage_layers(self):
+        b, e = C.c_int(), C.c_int()
+        n = lib.lvk_stage_layers(self.ctx, C.byref(b), C.byref(e))
+        return b.value, e.value, n
 
     def logits(self):
         rows = self._last_n if self.logits_all else 1
@@ -192,6 +224,17 @@ class Llama:
 
 
 # ---------------------------------------------------------------- operator level
+def model_hparams(path):
+    """ggjt/ggmf/ggml header hparams (n_vocab, n_embd, n_mult, n_head, n_layer, n_rot, ftype); llama.cpp:328-350"""
+    import struct
+    with open(path, "rb") as f:
+        head = f.read(40)
+    magic = struct.unpack("<I", head[:4])[0]
+    off = 4 if magic == 0x67676d6c else 8      # 'ggml' has no version field
+    return dict(zip(("n_vocab", "n_embd", "n_mult", "n_head", "n_layer", "n_rot", "ftype"),
+                    struct.unpack("<7I", head[off:off + 28])))
+
+
 def quantize_rows(x, qtype):
     x = np.ascontiguousarray(x, np.float32)
     n, k = x.shape
