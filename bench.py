@@ -40,6 +40,20 @@ def prompt_tokens(n):
     return [1] + [100 + (i * 7919) % 31000 for i in range(1, n)]
 
 
+class _StdoutToStderr:
+    """gloo prints connection notices on fd 1; the driver reads one JSON line there"""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *a):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def dist_setup():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -47,7 +61,8 @@ def dist_setup():
     pg = None
     if ws > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        with _StdoutToStderr():
+            dist.init_process_group("gloo")
         pg = dist
     return ws, rank, local, pg
 
@@ -114,12 +129,16 @@ def layer_split_decode(args, m_full, rank, ws, local, pg, n_ctx, ptoks):
     import torch.distributed as dist
     import lvk
     from pipeline import StagePipeline, layer_ranges
-    torch.cuda.set_device(local)
-    grp = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=120))
-    hp = lvk.model_hparams(args.model)
+    on_device = args.split_backend == "nccl"
+    dev = local % torch.cuda.device_count()
+    torch.cuda.set_device(dev)
+    with _StdoutToStderr():
+        grp = dist.new_group(backend=args.split_backend, timeout=datetime.timedelta(seconds=120))
+    path = args.split_model or args.model
+    hp = lvk.model_hparams(path)
     lr = layer_ranges(hp["n_layer"], ws)[rank]
-    st = lvk.Llama(args.model, n_ctx=n_ctx, layers=lr)
-    pipe = StagePipeline(st, hp["n_embd"], n_ctx, dist, on_device=True, device="cuda:%d" % local, group=grp)
+    st = lvk.Llama(path, n_ctx=n_ctx, layers=lr)
+    pipe = StagePipeline(st, hp["n_embd"], n_ctx, dist, on_device=on_device, device="cuda:%d" % dev, group=grp)
     lg = pipe.eval(list(ptoks), 0)
     tok = pipe.greedy_next(lg)
     n_past = len(ptoks)
@@ -140,9 +159,10 @@ def layer_split_decode(args, m_full, rank, ws, local, pg, n_ctx, ptoks):
     st.close()
     return {"value": args.steps_split / dt, "unit": "tok/s", "stages": ws, "steps": args.steps_split,
             "layers_per_stage": [list(x) for x in layer_ranges(hp["n_layer"], ws)],
-            "workload": "LLaMA-7B Q4_0 greedy decode, layers split over %d GPUs (one stage per GPU), "
-                        "residual stream f32 [4096] per token over RCCL send/recv; the 65B split is "
-                        "bench.py --split-only with a 65B file" % ws,
+            "workload": "%s greedy decode, layers split over %d ranks (one stage per rank), residual "
+                        "stream f32 [n_embd] per token over %s send/recv"
+                        % (os.path.basename(path), ws, "RCCL" if on_device else "gloo (host)"),
+            "n_embd": hp["n_embd"], "n_layer": hp["n_layer"],
             "ms_per_token": dt / args.steps_split * 1e3}
 
 
@@ -159,6 +179,9 @@ def main():
     ap.add_argument("--steps-13b", type=int, default=96)
     ap.add_argument("--no-split", action="store_true", help="N>1: skip the layer-split pipeline line (SURVEY 8e)")
     ap.add_argument("--steps-split", type=int, default=64)
+    ap.add_argument("--split-model", default=None, help="model for the layer-split line (default: the 7B file)")
+    ap.add_argument("--split-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="stage hand-off transport: RCCL on device buffers, or gloo through host memory")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
     args = ap.parse_args()

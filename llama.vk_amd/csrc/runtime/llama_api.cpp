@@ -199,7 +199,7 @@ static llama_context * init_context(const char * path_model, struct llama_contex
         c.model.hp.n_ctx = (uint32_t) params.n_ctx;
         if (!params.vocab_only) {
             c.init(params);
-            fprintf(stderr, "%s: kv self size  = %7.2f MB\n", __func__, c.kv_bytes() / 1024.0 / 1024.0);
+            fprintf(stderr, "llama_init_from_file: kv self size  = %7.2f MB\n", c.kv_bytes() / 1024.0 / 1024.0);
         }
     } catch (const lvk::Error & e) {
         fprintf(stderr, "error loading model: %s\n", e.msg.c_str());
