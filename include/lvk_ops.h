@@ -51,6 +51,12 @@ LVK_API int lvk_attention(const uint16_t * kc, const uint16_t * vc, const float 
 LVK_API int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
                                  int n_ctx, int n_past, int n, float * out, float * scores_out);
 
+/* Self-check of the softmax exp: the number of arguments h <= 0 (fp16 bits)
+ * where the device's computed fp16(expf(h)) differs from this host's
+ * table_exp_f16[h] (ggml.c:2915-2927).  Contexts use the computed exp only when
+ * this is 0 (env LVK_EXP_TABLE forces the table).  -1 on error. */
+LVK_API int lvk_exp_table_mismatches(void);
+
 /* y[t] = g * rms_norm(x[t]) (ggml.c:6024-6080 + llama.cpp:984) */
 LVK_API int lvk_rms_norm_mul(const float * x, const float * g, int k, int n, float * y);
 

@@ -24,6 +24,18 @@ namespace lvk {
 
 namespace {
 
+#ifdef LVK_PROBE_TIMING   // dev probe builds only: per-wave s_memtime trace of the attention kernel
+__device__ unsigned long long g_atrace[64 * 4 * 16];
+#define LVK_AT(ev)                                                                                    \
+    do {                                                                                              \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                   \
+        if ((threadIdx.x & 63) == 0 && blockIdx.y == 0)                                               \
+            g_atrace[((blockIdx.x * 2 + blockIdx.z) & 63) * 64 + (threadIdx.x >> 6) * 16 + (ev)] = t_; \
+    } while (0)
+#else
+#define LVK_AT(ev) do { } while (0)
+#endif
+
 __device__ __forceinline__ void unpack8h(const uint4 v, float f[8]) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -31,6 +43,12 @@ __device__ __forceinline__ void unpack8h(const uint4 v, float f[8]) {
         f[2 * k] = f16_to_f32((uint16_t) (w[k] & 0xFFFFu));
         f[2 * k + 1] = f16_to_f32((uint16_t) (w[k] >> 16));
     }
+}
+
+// one 1 KiB LDS-DMA piece per wave: lane l moves 16 bytes from src to
+// lds + 16*l (global_load_lds_dwordx4, no VGPR destination)
+__device__ __forceinline__ void dma16(const void * src, uint8_t * lds) {
+    __builtin_amdgcn_global_load_lds((const void *) src, (__attribute__((address_space(3))) void *) lds, 16, 0, 0);
 }
 
 // reduce the quad's 4x8 accumulators in the AVX2 F32Cx8_REDUCE order
@@ -47,6 +65,22 @@ __device__ __forceinline__ float quad_f16dot_reduce(const float s[8]) {
     return (t0 + t1) + (t2 + t3);                  // hadd, hadd
 }
 
+// table_exp_f16[h] (ggml.c:2915-2927: fp16(expf(fp16->f32(h)))) for the
+// arguments softmax produces (h <= 0, not NaN), computed in double and rounded
+// to f32 then f16 -- the two roundings the table went through.  Used only when
+// exp_check() has shown it equal to the uploaded host table on every such h.
+__device__ __forceinline__ uint16_t exp_h(uint16_t hx, const uint16_t * __restrict__ tab, bool computed) {
+    if (computed && ((hx & 0x8000u) || hx == 0) && (hx & 0x7fffu) <= 0x7c00u)
+        return f32_to_f16((float) exp((double) f16_to_f32(hx)));
+    return tab[hx];
+}
+
+__global__ void k_exp_check(const uint16_t * __restrict__ tab, int * __restrict__ bad) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h < 65536u && ((h & 0x8000u) || h == 0) && (h & 0x7fffu) <= 0x7c00u)
+        if (exp_h((uint16_t) h, tab, true) != tab[h]) atomicAdd(bad, 1);
+}
+
 // ---------------------------------------------------------------------------
 // Fused attention for one (token t, head h, half of the head dims):
 //   phase 1  scores of every position p < n_kv into LDS (quad = one position,
@@ -61,7 +95,7 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
                                               const uint16_t * __restrict__ vc, const uint16_t * __restrict__ exp_tab,
                                               ActQ out, const StepParams * sp, int E, int n_ctx, float scale,
                                               float * __restrict__ scores_dbg, float * __restrict__ out_f32,
-                                              uint16_t * __restrict__ p16_out) {
+                                              uint16_t * __restrict__ p16_out, int exp_computed) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NSTEP = HD / 32;
     const int n_past = sp->n_past, N = sp->n_tokens;
@@ -75,7 +109,11 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
     double * redd = (double *) (smem + (size_t) n_ctx * 6 + 32);   // 4 doubles
     const int lim = n_past + t;                                    // last unmasked position
 
-    // ---- phase 1: KQ (ggml_vec_dot_f16 over HD, Q in f16) ----
+    // ---- all global loads first: Q, the first 512 positions of K (8 passes of
+    // 64 positions, a lane quad per position) and of V (16 steps of 32
+    // positions for this thread's output dim).  Nothing here depends on the
+    // softmax, so one memory round trip covers the whole kernel at n_kv <= 512.
+    constexpr int KP = 8, VS = 16, PB = KP * 64;
     uint4 qv[NSTEP];
     {
         const uint4 * qp = (const uint4 *) (q16 + (size_t) t * E + h * HD) + r;
@@ -83,29 +121,56 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
         for (int st = 0; st < NSTEP; ++st) qv[st] = qp[st * 4];
     }
     const int npos = min(n_kv, lim + 1);     // masked positions get -inf without a dot
-    for (int p0 = 0; p0 < npos; p0 += 128) {
-        uint4 kv0[NSTEP], kv1[NSTEP];
-        const int pa = min(p0 + (tid >> 2), npos - 1), pb = min(p0 + 64 + (tid >> 2), npos - 1);
-        const uint4 * ka = (const uint4 *) (kc + (size_t) pa * E + h * HD) + r;
-        const uint4 * kb = (const uint4 *) (kc + (size_t) pb * E + h * HD) + r;
+    uint4 kv[KP][NSTEP];
+    auto load_k = [&](int pb) {
 #pragma unroll
-        for (int st = 0; st < NSTEP; ++st) { kv0[st] = ka[st * 4]; kv1[st] = kb[st * 4]; }
+        for (int ps = 0; ps < KP; ++ps) {
+            if (pb + ps * 64 < npos) {          // wave-uniform: no duplicate requests past n_kv
+                const int pp = min(pb + ps * 64 + (tid >> 2), npos - 1);
+                const uint4 * kp = (const uint4 *) (kc + (size_t) pp * E + h * HD) + r;
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-            for (int st = 0; st < NSTEP; ++st) {
-                float kf[8], qf[8];
-                unpack8h(hh ? kv1[st] : kv0[st], kf);
-                unpack8h(qv[st], qf);
-#pragma unroll
-                for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(kf[l], qf[l], s[l]);
+                for (int st = 0; st < NSTEP; ++st) kv[ps][st] = kp[st * 4];
             }
-            const float kq = quad_f16dot_reduce(s);
-            const int p = p0 + hh * 64 + (tid >> 2);
-            if (r == 0 && p < npos) sc[p] = kq * scale;      // ggml_vec_scale_f32 (llama.cpp:1026)
+        }
+    };
+    const int d = half * (HD / 2) + (tid >> 2);
+    const uint16_t * vrow = vc + (size_t) (h * HD + d) * n_ctx;
+    const int np = n_kv & ~31;
+    const int nvs = (n_kv + 31) / 32;                  // V steps including a partial one
+    // V steps 0..VS-1 go to LDS by DMA: step s of the workgroup's 64 dims is
+    // 4 KiB at vlds + s*4096, thread tid's 16 bytes at + tid*16
+    uint8_t * vlds = smem + (size_t) n_ctx * 6 + 64;
+    LVK_AT(0);
+    load_k(0);
+    {
+        uint8_t * vl = vlds + (tid & ~63) * 16;       // wave-uniform base
+        const int nd = min(nvs, VS);
+        for (int st = 0; st < nd; ++st) dma16(vrow + (size_t) st * 32 + r * 8, vl + st * 4096);
+    }
+    LVK_AT(1);
+
+    // ---- phase 1: KQ (ggml_vec_dot_f16 over HD, Q in f16) ----
+    for (int pb = 0; pb < npos; pb += PB) {
+        if (pb > 0) load_k(pb);
+#pragma unroll
+        for (int ps = 0; ps < KP; ++ps) {
+            if (pb + ps * 64 < npos) {
+                float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                for (int st = 0; st < NSTEP; ++st) {
+                    float kf[8], qf[8];
+                    unpack8h(kv[ps][st], kf);
+                    unpack8h(qv[st], qf);
+#pragma unroll
+                    for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(kf[l], qf[l], s[l]);
+                }
+                const float kq = quad_f16dot_reduce(s);
+                const int pp = pb + ps * 64 + (tid >> 2);
+                if (r == 0 && pp < npos) sc[pp] = kq * scale;      // ggml_vec_scale_f32 (llama.cpp:1026)
+            }
         }
     }
+    LVK_AT(2);
     for (int p = npos + tid; p < n_kv; p += 256) sc[p] = -INFINITY;   // ggml.c:7028-7031
     __syncthreads();
     if (scores_dbg && half == 0)
@@ -114,7 +179,7 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
     // ---- phase 2: softmax (ggml.c:7099-7121) ----
     float mx = -INFINITY;
     for (int p = tid; p < n_kv; p += 256) { const float v = sc[p]; mx = v > mx ? v : mx; }
-    mx = warp_max(mx);
+    mx = wave_max_f(mx);
     if (lane == 0) red[wave] = mx;
     __syncthreads();
     {
@@ -126,12 +191,12 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
         const float v = sc[p];
         float e = 0.0f;
         if (v != -INFINITY) {
-            e = f16_to_f32(exp_tab[f32_to_f16(v - mx)]);
+            e = f16_to_f32(exp_h(f32_to_f16(v - mx), exp_tab, exp_computed != 0));
             sum += (double) e;
         }
         sc[p] = e;
     }
-    sum = warp_sum_d(sum);
+    sum = wave_sum_d(sum);     // any order: the sum is exact
     if (lane == 0) redd[wave] = sum;
     __syncthreads();
     sum = (redd[0] + redd[1]) + (redd[2] + redd[3]);
@@ -142,39 +207,53 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
     if (p16_out && half == 0)
         for (int p = tid; p < n_kv; p += 256) p16_out[((size_t) t * gridDim.x + h) * n_ctx + p] = p16[p];
 
+    LVK_AT(3);
     // ---- phase 3: KQV = ggml_vec_dot_f16(n_kv, V row, P) ----
-    const int d = half * (HD / 2) + (tid >> 2);
-    const uint16_t * vrow = vc + (size_t) (h * HD + d) * n_ctx;
-    const int np = n_kv & ~31;
+    __syncthreads();     // vmcnt(0) + barrier: every wave's V DMA has landed
     const int nsteps = min(np, lim + 1 + 31) / 32;     // steps holding at least one unmasked position
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i0 = 0; i0 < nsteps; i0 += 8) {
-        uint4 vv[8];
+    auto pv_step = [&](const uint4 v4, int st) {
+        float vf[8], pf[8];
+        unpack8h(v4, vf);
+        unpack8h(*((const uint4 *) (p16 + st * 32) + r), pf);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) vv[u] = *((const uint4 *) (vrow + min(i0 + u, nsteps - 1) * 32) + r);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            if (i0 + u < nsteps) {
-                float vf[8], pf[8];
-                unpack8h(vv[u], vf);
-                unpack8h(*((const uint4 *) (p16 + (i0 + u) * 32) + r), pf);
-#pragma unroll
-                for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(vf[l], pf[l], s[l]);
-            }
-        }
-    }
+        for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(vf[l], pf[l], s[l]);
+    };
+    const int nl = min(nsteps, VS);
+    for (int st = 0; st < nl; ++st) pv_step(*((const uint4 *) (vlds + (size_t) st * 4096) + tid), st);
+    for (int st = VS; st < nsteps; ++st) pv_step(*((const uint4 *) (vrow + (size_t) st * 32) + r), st);
     const float res = quad_f16dot_reduce(s);
     float o = res;
-    if (r == 0) {
-        double sumf = (double) res;               // leftovers in double (ggml.c:1806-1808)
-        for (int i = np; i < n_kv && i <= lim; ++i) {
-            const float pr = f16_to_f32(vrow[i]) * f16_to_f32(p16[i]);
-            sumf += (double) pr;
+    if (np < n_kv && np <= lim) {
+        // leftovers in double, in position order (ggml.c:1806-1808), from registers
+        const int ts = np / 32;
+        uint4 vt[4], pt[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            pt[k] = *((const uint4 *) (p16 + np) + k);
+            if (ts < VS) vt[k] = *((const uint4 *) (vlds + (size_t) ts * 4096) + (tid & ~3) + k);
         }
-        o = (float) sumf;
+        if (ts >= VS)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) vt[k] = *((const uint4 *) (vrow + np) + k);
+        if (r == 0) {
+            const int nt_ = min(n_kv, lim + 1) - np;
+            double sumf = (double) res;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float vf[8], pf[8];
+                unpack8h(vt[k], vf);
+                unpack8h(pt[k], pf);
+#pragma unroll
+                for (int l = 0; l < 8; ++l)
+                    if (8 * k + l < nt_) { const float pr = vf[l] * pf[l]; sumf += (double) pr; }
+            }
+            o = (float) sumf;
+        }
     }
     if (r == 0 && out_f32) out_f32[(size_t) t * E + h * HD + d] = o;
 
+    LVK_AT(4);
     // ---- phase 4: quantize HD/2 outputs = HD/64 weight blocks ----
     __syncthreads();
     float * ob = sc;
@@ -217,9 +296,21 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
             }
         }
     }
+    LVK_AT(5);
 }
 
 }  // namespace
+
+#ifdef LVK_PROBE_TIMING
+void * lvk_probe_atrace() { void * p = nullptr; (void) hipGetSymbolAddress(&p, HIP_SYMBOL(g_atrace)); return p; }
+#endif
+
+hipError_t exp_check(const uint16_t * exp_tab, int * bad_d, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(bad_d, 0, sizeof(int), s);
+    if (e != hipSuccess) return e;
+    k_exp_check<<<256, 256, 0, s>>>(exp_tab, bad_d);
+    return hipGetLastError();
+}
 
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s) {
     const int hd = A.n_embd / A.n_head;
@@ -227,13 +318,14 @@ hipError_t launch_attention(const AttnLaunch & A, hipStream_t s) {
     if (A.out_qtype != Q4_0 && A.out_qtype != Q4_1) return hipErrorNotSupported;
     const float scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
     dim3 grid(A.n_head, A.n_tokens, 2);
-    const size_t lds = (size_t) A.n_ctx * 6 + 64;
+    // scores, P16, reductions, then V steps 0..15 by DMA (4 KiB each)
+    const size_t lds = (size_t) A.n_ctx * 6 + 64 + 16 * 4096;
     if (A.out_qtype == Q4_1)
         LVK_LAUNCH((k_attn<128, Q4_1>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,
-                   A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out);
+                   A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out, A.exp_computed);
     else
         LVK_LAUNCH((k_attn<128, Q4_0>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,
-                   A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out);
+                   A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out, A.exp_computed);
     return hipGetLastError();
 }
 

@@ -93,6 +93,20 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     }
     return (r[0] + r[1]) + (r[2] + r[3]);
 }
+// whole-wave float max through DPP + readlanes (max is exact in any order)
+__device__ __forceinline__ float wave_max_f(float v) {
+    auto mx = [](float a, float b) { return b > a ? b : a; };
+    v = mx(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false)));
+    v = mx(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)));
+    v = mx(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false)));
+    v = mx(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false)));
+    const int i = __builtin_bit_cast(int, v);
+    const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(i, 0));
+    const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(i, 16));
+    const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(i, 32));
+    const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(i, 48));
+    return mx(mx(r0, r1), mx(r2, r3));
+}
 __device__ __forceinline__ float warp_max(float v) {
     for (int o = 32; o > 0; o >>= 1) { const float w = __shfl_xor(v, o); v = w > v ? w : v; }
     return v;

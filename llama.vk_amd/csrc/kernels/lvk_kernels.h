@@ -123,8 +123,12 @@ struct AttnLaunch {
     int n_tokens, n_embd, n_head, n_ctx;
     float * out_f32 = nullptr; // optional: also store the unquantized merged heads [N][E]
     uint16_t * p16_out = nullptr; // optional (debug): f16 probabilities [N][H][n_ctx]
+    int exp_computed = 0;     // 1: softmax computes exp in registers (only after exp_check found 0 mismatches)
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
+// count (into *bad_d) the softmax arguments h <= 0 whose computed exp differs
+// from exp_tab[h]; 0 means the computed path reproduces the host table exactly
+hipError_t exp_check(const uint16_t * exp_tab, int * bad_d, hipStream_t s);
 
 // one-time weight repack: file-layout rows (ggml blocks) -> quad-sliced image
 // interleave4: src_rows holds two (M/2)-row matrices A then B; the image

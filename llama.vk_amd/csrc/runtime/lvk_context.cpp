@@ -90,6 +90,16 @@ void Context::init(const llama_context_params & p) {
     silu_tab = (uint16_t *) model.alloc(65536 * 2);
     LVK_HIP(hipMemcpy(exp_tab, te.data(), 65536 * 2, hipMemcpyHostToDevice));
     LVK_HIP(hipMemcpy(silu_tab, ts.data(), 65536 * 2, hipMemcpyHostToDevice));
+    {
+        // the softmax may compute exp instead of reading the table, but only if
+        // that reproduces this host's table on every argument it can see
+        int * bad_d = (int *) model.alloc(sizeof(int));
+        int bad = -1;
+        LVK_HIP(exp_check(exp_tab, bad_d, nullptr));
+        LVK_HIP(hipMemcpy(&bad, bad_d, sizeof(int), hipMemcpyDeviceToHost));
+        exp_computed = bad == 0 ? 1 : 0;
+        if (getenv("LVK_EXP_TABLE")) exp_computed = 0;
+    }
     // RoPE cos/sin table (ggml.c:7209-7213): theta = powf(10000, -i0/n_dims), angle = p*theta
     std::vector<float2> rt(C * (hd / 2));
     for (size_t pos = 0; pos < C; ++pos)
@@ -166,6 +176,7 @@ void Context::enqueue_forward(int n, bool last_only) {
         a.n_embd = E; a.head_dim = hd; a.n_ctx = n_ctx;
         timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
         AttnLaunch at{q16, kc + il * CE, vc + il * CE, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
+        at.exp_computed = exp_computed;
         timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
         MvLaunch b;
         b.w = ly.wo; b.xq = aq_attn; b.y = x; b.sp = sp_d; b.n_tokens = n;

@@ -39,6 +39,7 @@ struct Context {
     float * logits_d = nullptr;  // [n_ctx][V]
     float * emb_d = nullptr;     // [E]
     uint16_t * exp_tab = nullptr;
+    int exp_computed = 0;     // softmax exp computed in registers (verified equal to exp_tab)
     uint16_t * silu_tab = nullptr;
     float2 * rope = nullptr;     // [n_ctx][hd/2]
     StepParams * sp_d = nullptr;

@@ -162,6 +162,13 @@ int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float *
         std::vector<uint16_t> te, ts;
         lvk::host_fp16_tables(te, ts);
         A.exp_tab = dv.up(te.data(), te.size());
+        {
+            int * bad_d = (int *) dv.get(sizeof(int));
+            int bad = -1;
+            LVK_HIP(lvk::exp_check(A.exp_tab, bad_d, nullptr));
+            LVK_HIP(hipMemcpy(&bad, bad_d, sizeof(int), hipMemcpyDeviceToHost));
+            A.exp_computed = (bad == 0 && !getenv("LVK_EXP_TABLE")) ? 1 : 0;
+        }
         A.sp = dv.up(&sp, 1);
         A.n_tokens = n; A.n_embd = n_embd; A.n_head = n_head; A.n_ctx = n_ctx;
         float * od = (float *) dv.get((size_t) n * n_embd * 4);
@@ -179,6 +186,22 @@ int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float *
         }
         return 0;
     } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
+int lvk_exp_table_mismatches(void) {
+    try {
+        Dev dv;
+        std::vector<uint16_t> te, ts;
+        lvk::host_fp16_tables(te, ts);
+        const uint16_t * tab = dv.up(te.data(), te.size());
+        int * bad_d = (int *) dv.get(sizeof(int));
+        int bad = -1;
+        LVK_HIP(lvk::exp_check(tab, bad_d, nullptr));
+        LVK_HIP(hipMemcpy(&bad, bad_d, sizeof(int), hipMemcpyDeviceToHost));
+        return bad;
+    } catch (const std::exception & e) {
+        return fail("lvk_exp_table_mismatches", e.what());
+    }
 }
 
 int lvk_rms_norm_mul(const float * x, const float * g, int k, int n, float * y) {

@@ -87,6 +87,7 @@ _sig("lvk_mul_mat_q_norm", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, f32p, f32p,
 _sig("lvk_attention", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p])
 _sig("lvk_attention_scores", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p, f32p])
 _sig("lvk_rms_norm_mul", C.c_int, [f32p, f32p, C.c_int, C.c_int, f32p])
+_sig("lvk_exp_table_mismatches", C.c_int, [])
 _sig("lvk_host_tables", None, [u16p, u16p])
 _sig("lvk_set_profiling", None, [C.c_void_p, C.c_int])
 _sig("lvk_get_profile", C.c_int, [C.c_void_p, f64p, i64p, f64p, C.c_int])
@@ -277,6 +278,11 @@ def attention_scores(kc, vc, q, n_embd, n_head, n_ctx, n_past, n):
                                     out, sc), "lvk_attention_scores")
     p16 = sc[m:].view(np.uint16)[:m].reshape(n, n_head, n_ctx)
     return out, sc[:m].reshape(n, n_head, n_ctx), p16
+
+
+def exp_table_mismatches():
+    """Arguments h <= 0 where the device's computed exp differs from table_exp_f16."""
+    return int(lib.lvk_exp_table_mismatches())
 
 
 def rms_norm_mul(x, g):

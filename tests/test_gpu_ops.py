@@ -92,13 +92,27 @@ def test_mul_mat_q4_0_rmsnorm_prologue(lvk, oracle, m, k, n):
     assert np.array_equal(bits(got), bits(want))
 
 
-@pytest.mark.parametrize("n_past,N", [(0, 1), (5, 1), (31, 1), (32, 1), (200, 1), (40, 3), (60, 37), (0, 64), (10, 100)])
-def test_attention(lvk, oracle, n_past, N):
-    E, H, C = 512, 4, 256
-    rng = np.random.default_rng(n_past * 131 + N)
+def test_exp_self_check(lvk):
+    # the softmax computes fp16(expf(h)) in registers only when it equals this
+    # host's table_exp_f16 on every argument h <= 0; on this image it must
+    assert lvk.exp_table_mismatches() == 0
+
+
+@pytest.mark.parametrize("exp_path", ["computed", "table"])
+@pytest.mark.parametrize("n_past,N,C,qs", [(0, 1, 256, 1), (5, 1, 256, 1), (31, 1, 256, 1), (32, 1, 256, 1),
+                                           (200, 1, 256, 1), (40, 3, 256, 1), (60, 37, 256, 1), (0, 64, 256, 1),
+                                           (10, 100, 256, 1), (200, 1, 256, 8), (700, 1, 1024, 1),
+                                           (511, 2, 1024, 4), (1000, 3, 1024, 1)])
+def test_attention(lvk, oracle, monkeypatch, exp_path, n_past, N, C, qs):
+    # C = 1024 runs V steps past the 16 staged in LDS; qs scales q so the
+    # softmax reaches deep-negative exp arguments (fp16 underflow to 0)
+    if exp_path == "table":
+        monkeypatch.setenv("LVK_EXP_TABLE", "1")
+    E, H = 512, 4
+    rng = np.random.default_rng(n_past * 131 + N + C)
     kc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
     vc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
-    q = rng.standard_normal(N * E).astype(np.float32)
+    q = (qs * rng.standard_normal(N * E)).astype(np.float32)
     got = lvk.attention(kc, vc, q, E, H, C, n_past, N)
     want = np.zeros(N * E, np.float32)
     oracle.lib.orc_attention(kc, vc, q, E, H, C, n_past, N, want)

@@ -10,7 +10,7 @@
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1);} } while (0)
 using namespace lvk;
 #ifdef LVK_PROBE_TIMING
-namespace lvk { void * lvk_probe_trace(); }
+namespace lvk { void * lvk_probe_trace(); void * lvk_probe_atrace(); }
 #endif
 
 __global__ void k_fill_u32(uint32_t * p, size_t n, uint32_t seed) {
@@ -89,6 +89,7 @@ int main(int argc, char ** argv) {
             CK(mv(a, PRO_NORM, EPI_QKV));
         } else if (k == 1) {
             AttnLaunch at{q16, kc + (size_t) l * C * E, vc + (size_t) l * C * E, scores, aqa, Q4_0, etab, sp, 1, E, H, C};
+            at.exp_computed = getenv("LVK_EXP_TABLE") ? 0 : 1;   // timing only: random table
             CK(launch_attention(at, s));
         } else if (k == 2) {
             MvLaunch b; b.w = y.wo; b.xq = aqa; b.y = x; b.sp = sp; b.n_tokens = 1;
@@ -142,6 +143,26 @@ int main(int argc, char ** argv) {
 #ifdef LVK_PROBE_TIMING
     {
         const int kind = getenv("LVK_TRACE_KIND") ? atoi(getenv("LVK_TRACE_KIND")) : 5;
+        if (kind == 1) {
+            void * at = lvk_probe_atrace();
+            std::vector<unsigned long long> h(64 * 64);
+            for (int l = 0; l < 4; l++) op(1, l);
+            CK(hipStreamSynchronize(s));
+            CK(hipMemset(at, 0, h.size() * 8));
+            op(1, 4);
+            CK(hipStreamSynchronize(s));
+            CK(hipMemcpy(h.data(), at, h.size() * 8, hipMemcpyDeviceToHost));
+            double acc[6] = {0}; int n = 0;
+            for (int w = 0; w < 64 * 4; w++) {
+                unsigned long long * e = &h[(size_t) w * 16];
+                if (!e[0] || !e[5]) continue;
+                n++;
+                for (int k = 1; k < 6; k++) acc[k] += (double) (e[k] - e[0]);
+            }
+            printf("attention trace (%d waves): loads-issued %.0f  scores %.0f  softmax %.0f  pv %.0f  end %.0f cycles\n",
+                   n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+            return 0;
+        }
         void * tr = lvk_probe_trace();
         const size_t n = 256 * 16 * 64;
         std::vector<unsigned long long> h(n);
