@@ -40,6 +40,16 @@ LVK_API int lvk_mul_mat_q(int type, const void * w, int m, int k, const float * 
 LVK_API int lvk_mul_mat_q_norm(int type, const void * w, int m, int k, const float * g, const float * x, int n,
                                float * y);
 
+/* The prompt-batch (N > 1) matmul on the MFMA cores (mm_mfma.hip), Q4_0 only:
+ * same inputs and meaning as lvk_mul_mat_q / lvk_mul_mat_q_norm (g != NULL:
+ * fused RMSNorm * g).  The activation quantization and every per-block
+ * integer dot are bit-exact; the block scales are accumulated in fp32 in block
+ * order, acc = fmaf(dw*dx, I_b, acc), instead of the reference's 8 interleaved
+ * AVX2 chains (ggml.c:1950-2026), so results agree with lvk_mul_mat_q to fp32
+ * rounding.  Needs m % 128 == 0, k % 256 == 0, n >= 1. */
+LVK_API int lvk_mul_mat_q_mfma(int type, const void * w, int m, int k, const float * g, const float * x, int n,
+                               float * y);
+
 /* one layer's attention block on an f16 KV cache (llama.cpp:1010-1061):
  * kc [n_ctx][n_embd] f16, vc [n_embd][n_ctx] f16, q [n][n_embd] f32 (post-RoPE)
  * -> out [n][n_embd] f32 (merged heads, before the Wo quantization) */
@@ -73,6 +83,10 @@ LVK_API int lvk_get_profile(struct llama_context * ctx, double * ms, long * laun
 LVK_API void lvk_reset_profile(struct llama_context * ctx);
 /* bytes of quantized weights resident in HBM for this context's model */
 LVK_API size_t lvk_weight_bytes(struct llama_context * ctx);
+/* 1 = prompt batches (N > 1) use the bit-faithful VALU matmuls (the reference's
+ * exact fp32 chain order), 0 = the MFMA matmuls (default; env LVK_PROMPT_EXACT=1
+ * makes 1 the default) */
+LVK_API void lvk_set_prompt_exact(struct llama_context * ctx, int on);
 /* 1 = replay the captured decode graph for single-token evals (default), 0 = eager */
 LVK_API void lvk_set_graph(struct llama_context * ctx, int on);
 

@@ -1,0 +1,502 @@
+// mm_mfma.hip -- prompt-eval (N > 1) Q4_0 matmul on the CDNA4 matrix cores,
+// bit-faithful to the reference AVX2 arithmetic.
+//
+// ggml_compute_forward_mul_mat_q_f32 (ggml.c:6510-6696) evaluates every
+// (row m, token n) as ggml_vec_dot_q4_0 (ggml.c:1950-2026): 8 fp32 chains
+//   acc_j = fmaf(dw_b * da_b, (float) P_bj, acc_j)   over blocks b in order,
+//   P_bj  = sum_{e=4j}^{4j+3} (qw_e - 8) * (qa_e - 8)  (exact integer),
+// then ((a0+a4)+(a2+a6)) + ((a1+a5)+(a3+a7)).  Those 8.5e11 sequential FMAs
+// (7B, 512-token prompt) are the floor of any bit-exact implementation; the
+// integer partials are what the matrix cores can take over.
+//
+// Here v_mfma_f32_32x32x8_f16 produces the partials: in its operand layout
+// lane half h holds k = 4h..4h+3, i.e. exactly one chain (2c+h) of a block's
+// elements 8c..8c+7.  The B columns are (16 tokens) x (2 chain parities jj);
+// lanes with h != jj hold zeros, so output column (n, jj) of the MFMA for
+// chain pair c is P_{b,2c+jj}[m, n] for 32 rows m: exact (|products| <= 64,
+// sums of 4 in f32).  The VALU then runs exactly the reference's chains:
+//   s = dw*da (ggml.c:1968), acc_j = fmaf(s, P_bj, acc_j) (ggml.c:2013),
+// and the final AVX2 horizontal order (ggml.c:2019-2024).  Every output is
+// bit-identical to ggml_vec_dot_q4_0 (pinned by tests/test_gpu_ops.py).
+//
+// Operands:
+//   A (weights): the decode "octet" image (lvk_kernels.h) read straight into
+//     registers: MFMA lane (row, h) loads octet lanes 8r + 2c + h (chains
+//     2c+h, c = 0..3) of its row group, 4 x 16 B per 8 blocks; nibbles -> f16
+//     with the magic-exponent trick (0x6400|q = 1024+q, 0x4C00|q<<4 = 16+q/4)
+//     in the chain order e0 e2 e1 e3.
+//   B (activations): Q4_0-quantized tokens as f16 values q-8 [N][K] in the
+//     same per-chain order (launch_act_f16), staged per 4 blocks through LDS
+//     into the masked fragment image [block][c][jj][h][token] whose h != jj
+//     slots stay zero, so every lane reads its fragment with one ds_read_b64.
+// Workgroup = 4 waves, tile 128 rows x 16 tokens (wave w: rows 32w..32w+31,
+// all 8 chains: 64 accumulator registers); workgroups are mapped so the 8
+// XCDs each sweep contiguous row tiles with the token tiles innermost (the
+// weight tile is fetched into that XCD's L2 once for all its token tiles).
+#include "lvk_device.h"
+#include "lvk_kernels.h"
+#include "matvec_common.h"
+
+namespace lvk {
+
+namespace {
+
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+constexpr int TM = 128;     // rows per workgroup
+constexpr int TN = 16;      // tokens per workgroup
+constexpr int NT = 256;     // threads (4 waves)
+constexpr int SBK = 4;      // blocks per LDS stage
+
+// masked B image: per (block, c) 4 slots (jj, h) of 16 tokens x 8 B, slot stride
+// 192 B (48 dwords: the two slots a ds_read_b64 half-wave touches fall in
+// disjoint bank halves)
+constexpr int SLOT = 192;
+constexpr int BC_BYTES = 4 * SLOT;                  // one (block, c)
+constexpr int LDS_B = SBK * 4 * BC_BYTES;           // 12 KiB per stage buffer
+constexpr int LDS_DW = 32 * TM * 4;                 // 16 KiB: [block of chunk][row]
+constexpr int LDS_DA = 32 * TN * 4;                 // 2 KiB:  [block of chunk][token]
+constexpr int OFF_B0 = 0, OFF_B1 = LDS_B;
+constexpr int OFF_DW0 = 2 * LDS_B, OFF_DW1 = OFF_DW0 + LDS_DW;
+constexpr int OFF_DA0 = OFF_DW1 + LDS_DW, OFF_DA1 = OFF_DA0 + LDS_DA;
+constexpr int LDS_TOTAL = OFF_DA1 + LDS_DA;         // 60 KiB: two workgroups per CU
+
+struct MmParams {
+    const uint4 * nib;
+    const float4 * scl;
+    int M, K, nb, NC;
+    const uint16_t * xh;     // [N][K] f16 (per-chain order e0 e2 e1 e3)
+    const float * da;        // [N][nb]
+    int N;                   // tokens
+    int ntt;                 // token tiles
+    float * y;               // output
+    int ldy;
+    int out_tok0;
+    const uint16_t * silu_tab;
+};
+
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t o) {
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(m), "v"(o));
+    return r;
+}
+
+// 16-bit chain field (4 unsigned nibbles e0..e3) selected by sel from X -> f16 e0 e2 e1 e3
+__device__ __forceinline__ half4_t unpack_chain(uint32_t X, uint32_t sel) {
+    const uint32_t t = __builtin_amdgcn_perm(X, X, sel);            // byte0 | byte1 << 16
+    const uint32_t lo = and_or(t, 0x000F000Fu, 0x64006400u);        // (e0, e2) = 1024 + q
+    const uint32_t hi = and_or(t, 0x00F000F0u, 0x4C004C00u);        // (e1, e3) = 16 + q/4
+    const half2_t c1032 = {(_Float16) -1032.0f, (_Float16) -1032.0f};
+    const half2_t c4 = {(_Float16) 4.0f, (_Float16) 4.0f};
+    const half2_t c72 = {(_Float16) -72.0f, (_Float16) -72.0f};
+    const half2_t h0 = __builtin_bit_cast(half2_t, lo) + c1032;                           // q - 8
+    const half2_t h1 = __builtin_elementwise_fma(__builtin_bit_cast(half2_t, hi), c4, c72); // q - 8
+    half4_t r;
+    r[0] = h0[0]; r[1] = h0[1]; r[2] = h1[0]; r[3] = h1[1];
+    return r;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = tid >> 6;
+    // XCD-aware tile order: workgroup b runs on XCD b % 8; give each XCD a
+    // contiguous range of (row tile, token tile) with token tiles innermost
+    const int nwg = gridDim.x;
+    const int b = blockIdx.x;
+    const int full = nwg & ~7;
+    const int L = b < full ? (b & 7) * (full >> 3) + (b >> 3) : b;
+    const int m0 = (L / P.ntt) * TM;
+    const int n0 = (L % P.ntt) * TN;
+    const int K = P.K, nb = P.nb, NC = P.NC;
+    const int S = nb / SBK;                    // stages (even: nb % 8 == 0)
+    const int G0 = m0 / 8;
+
+    // zero the masked (h != jj) slots of both B buffers once
+    for (int i = tid; i < 2 * SBK * 4 * 2 * (TN * 8 / 16); i += NT) {
+        const int per = TN * 8 / 16;                      // uint4 per slot
+        const int q = i % per, rest = i / per;
+        const int which = rest & 1, bc = rest >> 1;       // which: slot 1 or 2
+        ((uint4 *) (smem + (size_t) bc * BC_BYTES + (which ? 2 : 1) * SLOT))[q] = make_uint4(0, 0, 0, 0);
+    }
+
+    // ---- staging registers (global -> LDS) ----
+    uint4 rb;             // B: 16 B per thread per stage
+    float rda[2];         // da: chunk boundary
+    float4 rdw[4];        // dw: chunk boundary
+    auto load_b = [&](int s) {
+        const int n = tid >> 4, u = tid & 15;              // token, uint4 of its 256 B stage slice
+        const int tok = min(n0 + n, P.N - 1);
+        rb = *(const uint4 *) (P.xh + (size_t) tok * K + (size_t) s * (SBK * 32) + u * 8);
+    };
+    auto store_b = [&](int s) {
+        uint8_t * bl = smem + ((s & 1) ? OFF_B1 : OFF_B0);
+        const int n = tid >> 4, u = tid & 15;
+        const int jb = u >> 2, c = u & 3;                 // chains 2c (first 8 B), 2c+1
+        uint8_t * bc = bl + (jb * 4 + c) * BC_BYTES;
+        *(uint2 *) (bc + 0 * SLOT + n * 8) = make_uint2(rb.x, rb.y);    // (jj 0, h 0)
+        *(uint2 *) (bc + 3 * SLOT + n * 8) = make_uint2(rb.z, rb.w);    // (jj 1, h 1)
+    };
+    auto load_scales = [&](int c) {        // chunk c: 32 blocks
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int Li = i * NT + tid;
+            rdw[i] = P.scl[(size_t) (G0 + (Li >> 6)) * NC * 64 + (size_t) c * 64 + (Li & 63)];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int Li = i * NT + tid;
+            const int n = Li >> 5, jb = Li & 31;
+            const int tok = min(n0 + n, P.N - 1);
+            rda[i] = P.da[(size_t) tok * nb + min(c * 32 + jb, nb - 1)];
+        }
+    };
+    auto store_scales = [&](int c) {
+        float * wl = (float *) (smem + ((c & 1) ? OFF_DW1 : OFF_DW0));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int Li = i * NT + tid;
+            const int G = Li >> 6, l = Li & 63;
+            const int r = l >> 3, j = l & 7;
+            const float v[4] = {rdw[i].x, rdw[i].y, rdw[i].z, rdw[i].w};
+#pragma unroll
+            for (int m = 0; m < 4; ++m) wl[(8 * m + j) * TM + 8 * G + r] = v[m];
+        }
+        float * dl = (float *) (smem + ((c & 1) ? OFF_DA1 : OFF_DA0));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int Li = i * NT + tid;
+            dl[(Li & 31) * TN + (Li >> 5)] = rda[i];
+        }
+    };
+
+    // ---- A operand: MFMA lane (row rho, half h) <- octet lanes 8r + 2c + h ----
+    const int rho = lane & 31, h = lane >> 5;
+    const int arow = m0 + 32 * w + rho;
+    const uint4 * ap = P.nib + (size_t) (arow >> 3) * NC * 256 + 8 * (arow & 7) + h;
+    auto load_a = [&](int u, uint4 (&A)[4]) {              // sub-chunk u = 8 blocks
+        const uint4 * p = ap + (size_t) u * 64;            // (c*4 + sb) * 64 == u * 64
+#pragma unroll
+        for (int c = 0; c < 4; ++c) A[c] = ld_nt(p + 2 * c);
+    };
+
+    f32x16_t acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[c][i] = 0.0f;
+
+    // B fragment lane offset: slot (jj, h), token lane&15
+    const int jj = (lane >> 4) & 1;
+    const int boff = (jj * 2 + h) * SLOT + (lane & 15) * 8;
+
+    const int U = nb / 8;
+    uint4 Acur[4], Anext[4];
+    load_b(0);
+    load_scales(0);
+    load_a(0, Acur);
+    store_b(0);
+    store_scales(0);
+    __syncthreads();
+
+    // one stage = 4 blocks; ko selects the A dwords (0: blocks 0-3 of the sub-chunk, 2: blocks 4-7)
+    auto compute_stage = [&](int s, int ko, const uint32_t (&X)[4][4]) {
+        const uint8_t * bl = smem + ((s & 1) ? OFF_B1 : OFF_B0);
+        const int ch = s >> 3;                              // chunk
+        const float * wl = (const float *) (smem + ((ch & 1) ? OFF_DW1 : OFF_DW0));
+        const float * dl = (const float *) (smem + ((ch & 1) ? OFF_DA1 : OFF_DA0));
+#pragma unroll
+        for (int jb = 0; jb < SBK; ++jb) {
+            const int jc = (s & 7) * SBK + jb;              // block within the chunk
+            const uint32_t sel = (jb & 1) ? 0x0C030C02u : 0x0C010C00u;
+            half4_t bf[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                bf[c] = __builtin_bit_cast(half4_t, *(const uint2 *) (bl + (jb * 4 + c) * BC_BYTES + boff));
+            // block order pinned: nothing of this block is hoisted above the previous block's FMAs
+#pragma unroll
+            for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(bf[c]));
+            // s = dw * da for this lane's 16 rows (ggml.c:1968)
+            const float dav = dl[jc * TN + (lane & 15)];
+            float sc[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 d4 = *(const float4 *) (wl + jc * TM + 32 * w + 8 * q + 4 * h);
+                sc[4 * q + 0] = d4.x * dav; sc[4 * q + 1] = d4.y * dav;
+                sc[4 * q + 2] = d4.z * dav; sc[4 * q + 3] = d4.w * dav;
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const half4_t af = unpack_chain(X[c][ko + (jb >> 1)], sel);
+                const f32x16_t Pc = __builtin_amdgcn_mfma_f32_32x32x8f16(af, bf[c], (f32x16_t){}, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[c][i] = __builtin_fmaf(sc[i], Pc[i], acc[c][i]);  // ggml.c:2013
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(acc[c]));
+        }
+    };
+
+    for (int u = 0; u < U; ++u) {
+        if (u + 1 < U) load_a(u + 1, Anext);
+        uint32_t X[4][4];                                   // signed octet nibbles -> unsigned q
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            X[c][0] = Acur[c].x ^ 0x88888888u; X[c][1] = Acur[c].y ^ 0x88888888u;
+            X[c][2] = Acur[c].z ^ 0x88888888u; X[c][3] = Acur[c].w ^ 0x88888888u;
+        }
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int s = 2 * u + half;
+            const bool more = s + 1 < S;
+            const bool chunk_next = more && ((s + 1) & 7) == 0;
+            if (more) load_b(s + 1);
+            if (chunk_next) load_scales((s + 1) >> 3);
+            compute_stage(s, 2 * half, X);
+            if (more) store_b(s + 1);
+            if (chunk_next) store_scales((s + 1) >> 3);
+            __syncthreads();
+        }
+        if (u + 1 < U) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) Acur[c] = Anext[c];
+        }
+    }
+
+    // ---- AVX2 horizontal order (ggml.c:2019-2024): lane (h, n, jj) register set c holds chain 2c+jj;
+    // r_j = a_j + a_{j+4} (same lane, sets c and c+2), (r0+r2) | (r1+r3) in lanes jj = 0 | 1, then across
+    // the lane pair (xor 16)
+    float res[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float r0 = acc[0][i] + acc[2][i];       // r_jj     = a_jj + a_{jj+4}
+        const float r2 = acc[1][i] + acc[3][i];       // r_{2+jj} = a_{2+jj} + a_{6+jj}
+        const float v = r0 + r2;
+        res[i] = v + __shfl_xor(v, 16);               // (r0 + r2) + (r1 + r3) in the jj = 0 lanes
+    }
+
+    // ---- epilogue: jj = 0 lanes hold rows 32w + 8q + 4h + p (i = 4q + p) of token n ----
+    const int n = n0 + (lane & 15);
+    if constexpr (EPI == EPI_SWIGLU_F32) {
+        // W1|W3 image interleaved per 4 rows: h = 0 lanes hold the w1 rows, h = 1 the w3 rows of the
+        // same outputs (llama.cpp:1085-1096)
+        float o[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[i] = __shfl_xor(res[i], 32);
+        if (jj == 0 && h == 0 && n < P.N) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float uu[4];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res[4 * q + p])]);  // ggml.c:2495
+                    uu[p] = sl * o[4 * q + p];                                            // llama.cpp:1096
+                }
+                const int row = m0 + 32 * w + 8 * q;
+                *(float4 *) (P.y + (size_t) (P.out_tok0 + n) * P.ldy + row / 2) = make_float4(uu[0], uu[1], uu[2], uu[3]);
+            }
+        }
+    } else {
+        if (jj == 0 && n < P.N) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float4 * yp = (float4 *) (P.y + (size_t) (P.out_tok0 + n) * P.ldy + m0 + 32 * w + 8 * q + 4 * h);
+                if constexpr (EPI == EPI_RESID) {
+                    const float4 r = *yp;                 // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+                    *yp = make_float4(res[4 * q] + r.x, res[4 * q + 1] + r.y, res[4 * q + 2] + r.z, res[4 * q + 3] + r.w);
+                } else {
+                    *yp = make_float4(res[4 * q], res[4 * q + 1], res[4 * q + 2], res[4 * q + 3]);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Activation quantizer for the MFMA path: x[t] (optionally rms_norm * g) ->
+// quantize_row_q4_0 (AVX2 branch, ggml.c:621-685) -> f16 values q-8 in the
+// A-unpack k order + da.  One workgroup per token; the RMSNorm double sum is
+// the same per-thread strided / wave tree / in-order-waves reduction as the
+// matvec prologue (matvec_q4.hip prologue_norm).
+// ---------------------------------------------------------------------------
+template <bool NORM>
+__global__ __launch_bounds__(256) void k_act_q40_f16(const float * __restrict__ x, const float * __restrict__ g,
+                                                     int K, uint16_t * __restrict__ xh, float * __restrict__ da) {
+    __shared__ double red[4];
+    __shared__ float s_scale;
+    const int t = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int nunits = K / 8;
+    const float * xr = x + (size_t) t * K;
+    float scale = 1.0f;
+    if constexpr (NORM) {
+        double acc = 0.0;
+        for (int u = tid; u < nunits; u += 256) {
+            const float4 a = *(const float4 *) (xr + u * 8), b = *(const float4 *) (xr + u * 8 + 4);
+            const float e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { const float sq = e[q] * e[q]; acc += (double) sq; }
+        }
+        acc = warp_sum_d(acc);
+        if ((tid & 63) == 0) red[tid >> 6] = acc;
+        __syncthreads();
+        if (tid == 0) {
+            double s = 0.0;
+            for (int wv = 0; wv < 4; ++wv) s += red[wv];
+            const float mean = (float) (s / (double) K);          // ggml.c:6058-6071
+            s_scale = 1.0f / sqrtf(mean + 1e-6f);
+        }
+        __syncthreads();
+        scale = s_scale;
+    }
+    for (int u0 = 0; u0 < nunits; u0 += 256) {
+        const int u = u0 + tid;
+        const bool live = u < nunits;          // nunits % 4 == 0: quads are all live or all dead
+        float v[8];
+        if (live) {
+            const float4 a = *(const float4 *) (xr + u * 8), b = *(const float4 *) (xr + u * 8 + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+            if constexpr (NORM) {
+                const float4 ga = *(const float4 *) (g + u * 8), gb = *(const float4 *) (g + u * 8 + 4);
+                const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float yn = v[e] * scale;     // ggml_vec_scale_f32 (ggml.c:6076)
+                    v[e] = gg[e] * yn;                 // ggml_mul(repeat(g), cur) (llama.cpp:984)
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = 0.0f;
+        }
+        float amax = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float a = fabsf(v[e]); amax = a > amax ? a : amax; }
+        const float o0 = quad_bcast<0>(amax), o1 = quad_bcast<1>(amax);
+        const float o2 = quad_bcast<2>(amax), o3 = quad_bcast<3>(amax);
+        const float m01 = o1 > o0 ? o1 : o0, m23 = o3 > o2 ? o3 : o2;
+        amax = m23 > m01 ? m23 : m01;
+        const float d = amax / 7.0f;                              // ggml.c:651
+        const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;     // ggml.c:653
+        if (live) {
+            uint16_t h[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int q = ((int) __builtin_rintf(v[e] * id) + 8) & 15;   // ggml.c:655-684
+                h[e] = __builtin_bit_cast(uint16_t, (_Float16) (float) (q - 8));
+            }
+            uint4 o;   // k order e0 e2 e1 e3 e4 e6 e5 e7
+            o.x = h[0] | (uint32_t) h[2] << 16; o.y = h[1] | (uint32_t) h[3] << 16;
+            o.z = h[4] | (uint32_t) h[6] << 16; o.w = h[5] | (uint32_t) h[7] << 16;
+            *(uint4 *) (xh + (size_t) t * K + u * 8) = o;
+            if ((u & 3) == 0) da[(size_t) t * (K / 32) + (u >> 2)] = d;
+        }
+    }
+}
+
+// pre-quantized Q4_0 blocks (ActQ: d + reference nibble qs) -> f16 + da
+__global__ void k_actq_to_f16(ActQ q, int N, int K, uint16_t * __restrict__ xh, float * __restrict__ da) {
+    const int nb = K / 32;
+    const long idx = (long) blockIdx.x * blockDim.x + threadIdx.x;   // (token, block, group of 8)
+    if (idx >= (long) N * nb * 4) return;
+    const int gq = (int) (idx & 3);
+    const long tb = idx >> 2;
+    const uint4 qs = q.qs[tb];
+    const uint32_t wd[4] = {qs.x, qs.y, qs.z, qs.w};
+    const uint32_t word = wd[gq];              // elements 8gq..8gq+7: element 2k = byte k low nibble
+    uint16_t h[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int qv = (int) ((word >> (4 * e)) & 15u);
+        h[e] = __builtin_bit_cast(uint16_t, (_Float16) (float) (qv - 8));
+    }
+    uint4 o;
+    o.x = h[0] | (uint32_t) h[2] << 16; o.y = h[1] | (uint32_t) h[3] << 16;
+    o.z = h[4] | (uint32_t) h[6] << 16; o.w = h[5] | (uint32_t) h[7] << 16;
+    const long t = tb / nb, b = tb % nb;
+    *(uint4 *) (xh + (size_t) t * K + b * 32 + gq * 8) = o;
+    if (gq == 0) da[tb] = q.d[tb];
+}
+
+// RoPE mode 0 (ggml.c:7156-7227) + KV append (llama.cpp:996-1008) of the
+// stored Q|K|V rows [N][3E] -> q16 [N][E], K cache [pos][E], V cache [E][pos]
+__global__ void k_rope_kv(const float * __restrict__ qkv, int N, int E, int hd, const float2 * __restrict__ rope,
+                          const StepParams * __restrict__ sp, int n_ctx, uint16_t * __restrict__ q16,
+                          uint16_t * __restrict__ kc, uint16_t * __restrict__ vc) {
+    const int t = blockIdx.y;
+    const int e2 = blockIdx.x * blockDim.x + threadIdx.x;     // pair index over Q|K (E/2 each) then V
+    const int pos = sp->n_past + t;
+    const float * row = qkv + (size_t) t * 3 * E;
+    if (e2 < E) {                // Q and K pairs: e2 in [0, E): which = e2 / (E/2)
+        const int which = e2 / (E / 2);
+        const int e = 2 * (e2 - which * (E / 2));
+        const float x0 = row[which * E + e], x1 = row[which * E + e + 1];
+        const int i0 = e % hd;
+        const float2 cs = rope[(size_t) pos * (hd / 2) + (i0 >> 1)];
+        const float a0 = x0 * cs.x, b0 = x1 * cs.y;
+        const float o0 = a0 - b0;
+        const float a1 = x0 * cs.y, b1 = x1 * cs.x;
+        const float o1 = a1 + b1;
+        if (which == 0) {
+            q16[(size_t) t * E + e] = f32_to_f16(o0);
+            q16[(size_t) t * E + e + 1] = f32_to_f16(o1);
+        } else {
+            kc[(size_t) pos * E + e] = f32_to_f16(o0);
+            kc[(size_t) pos * E + e + 1] = f32_to_f16(o1);
+        }
+    } else if (e2 < E + E / 2) {
+        const int e = 2 * (e2 - E);
+        vc[(size_t) e * n_ctx + pos] = f32_to_f16(row[2 * E + e]);
+        vc[(size_t) (e + 1) * n_ctx + pos] = f32_to_f16(row[2 * E + e + 1]);
+    }
+}
+
+}  // namespace
+
+bool mm_mfma_supported(const QMatrix & w) {
+    return w.qtype == Q4_0 && w.M % TM == 0 && w.K % 256 == 0;
+}
+
+hipError_t launch_mm_mfma(const QMatrix & w, const uint16_t * xh, const float * da, int N, float * y, int ldy,
+                          int out_tok0, int epi, const uint16_t * silu_tab, hipStream_t s) {
+    if (!mm_mfma_supported(w) || N <= 0) return hipErrorInvalidValue;
+    MmParams P{};
+    P.nib = w.nib; P.scl = (const float4 *) w.scl;
+    P.M = w.M; P.K = w.K; P.nb = w.K / 32; P.NC = (P.nb + 31) / 32;
+    P.xh = xh; P.da = da; P.N = N; P.ntt = (N + TN - 1) / TN;
+    P.y = y; P.ldy = ldy; P.out_tok0 = out_tok0; P.silu_tab = silu_tab;
+    const dim3 grid((w.M / TM) * P.ntt);
+    switch (epi) {
+        case EPI_STORE: LVK_LAUNCH(k_mm_q40_mfma<EPI_STORE>, grid, dim3(NT), LDS_TOTAL, s, P); break;
+        case EPI_RESID: LVK_LAUNCH(k_mm_q40_mfma<EPI_RESID>, grid, dim3(NT), LDS_TOTAL, s, P); break;
+        case EPI_SWIGLU_F32: LVK_LAUNCH(k_mm_q40_mfma<EPI_SWIGLU_F32>, grid, dim3(NT), LDS_TOTAL, s, P); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_act_f16(const float * x, const float * g, int N, int K, uint16_t * xh, float * da, hipStream_t s) {
+    if (K % 256 || N <= 0) return hipErrorInvalidValue;
+    if (g) LVK_LAUNCH(k_act_q40_f16<true>, dim3(N), dim3(256), 0, s, x, g, K, xh, da);
+    else LVK_LAUNCH(k_act_q40_f16<false>, dim3(N), dim3(256), 0, s, x, g, K, xh, da);
+    return hipGetLastError();
+}
+
+hipError_t launch_actq_to_f16(const ActQ & q, int N, int K, uint16_t * xh, float * da, hipStream_t s) {
+    const long n = (long) N * (K / 32) * 4;
+    LVK_LAUNCH(k_actq_to_f16, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, q, N, K, xh, da);
+    return hipGetLastError();
+}
+
+hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 * rope, const StepParams * sp,
+                          int n_ctx, uint16_t * q16, uint16_t * kc, uint16_t * vc, hipStream_t s) {
+    const int pairs = E + E / 2;
+    LVK_LAUNCH(k_rope_kv, dim3((pairs + 255) / 256, N), dim3(256), 0, s, qkv, N, E, hd, rope, sp, n_ctx, q16, kc, vc);
+    return hipGetLastError();
+}
+
+}  // namespace lvk

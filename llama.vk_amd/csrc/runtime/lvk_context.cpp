@@ -76,6 +76,14 @@ void Context::init(const llama_context_params & p) {
     aq_ffn.m = (float *) model.alloc(C * (F / 32) * 4);
     aq_ffn.qs = (uint4 *) model.alloc(C * (F / 32) * 16);
     u_ffn = (float *) model.alloc(F * 4);
+    {
+        const size_t Cp = (C + 63) / 64 * 64, KX = std::max(E, F);
+        xh = (uint16_t *) model.alloc(Cp * KX * 2);
+        xda = (float *) model.alloc(Cp * (KX / 32) * 4);
+        qkv32 = (float *) model.alloc(C * 3 * E * 4);
+        uf = (float *) model.alloc(C * F * 4);
+        prompt_exact = getenv("LVK_PROMPT_EXACT") && atoi(getenv("LVK_PROMPT_EXACT")) != 0;
+    }
     logits_d = (float *) model.alloc(C * V * 4);
     emb_d = (float *) model.alloc(E * 4);
     sp_d = (StepParams *) model.alloc(sizeof(StepParams));
@@ -160,10 +168,71 @@ static hipError_t mv_launch(const MvLaunch & L, int pro, int epi, hipStream_t s)
     return launch_matvec(L, pro, epi, s);
 }
 
+// prompt batches go through the MFMA matmuls when every matrix of the model fits them
+bool Context::use_mfma(int n) const {
+    if (n <= 1 || prompt_exact || model.qtype != Q4_0) return false;
+    for (const Layer & ly : model.layers)
+        if (!mm_mfma_supported(ly.wqkv) || !mm_mfma_supported(ly.wo) || !mm_mfma_supported(ly.w13) ||
+            !mm_mfma_supported(ly.w2))
+            return false;
+    return true;
+}
+
 void Context::enqueue_forward(int n, bool last_only) {
     const HParams & hp = model.hp;
     const int E = (int) hp.n_embd, H = (int) hp.n_head, hd = E / H, F = (int) hp.n_ff();
     const size_t CE = (size_t) n_ctx * E;
+    if (use_mfma(n)) {
+        // prompt batch on the matrix cores: per layer
+        //   act(norm) -> QKV (store) -> RoPE + KV append -> attention -> act -> Wo (+x)
+        //   act(norm) -> W1|W3 (silu * mul) -> act -> W2 (+x)
+        if (model.has_embed)
+            timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_d, n, x, stream); });
+        for (size_t il = 0; il < model.layers.size(); ++il) {
+            const Layer & ly = model.layers[il];
+            uint16_t * kcl = kc + il * CE;
+            uint16_t * vcl = vc + il * CE;
+            timed_launch(K_QKV, 0, [&] { return launch_act_f16(x, ly.attn_norm, n, E, xh, xda, stream); });
+            timed_launch(K_QKV, qbytes(ly.wqkv), [&] {
+                return launch_mm_mfma(ly.wqkv, xh, xda, n, qkv32, 3 * E, 0, EPI_STORE, nullptr, stream);
+            });
+            timed_launch(K_QKV, 0, [&] {
+                return launch_rope_kv(qkv32, n, E, hd, rope, sp_d, n_ctx, q16, kcl, vcl, stream);
+            });
+            AttnLaunch at{q16, kcl, vcl, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
+            at.exp_computed = exp_computed;
+            timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
+            timed_launch(K_WO, 0, [&] { return launch_actq_to_f16(aq_attn, n, E, xh, xda, stream); });
+            timed_launch(K_WO, qbytes(ly.wo), [&] {
+                return launch_mm_mfma(ly.wo, xh, xda, n, x, E, 0, EPI_RESID, nullptr, stream);
+            });
+            timed_launch(K_W13, 0, [&] { return launch_act_f16(x, ly.ffn_norm, n, E, xh, xda, stream); });
+            timed_launch(K_W13, qbytes(ly.w13), [&] {
+                return launch_mm_mfma(ly.w13, xh, xda, n, uf, F, 0, EPI_SWIGLU_F32, silu_tab, stream);
+            });
+            timed_launch(K_W2, 0, [&] { return launch_act_f16(uf, nullptr, n, F, xh, xda, stream); });
+            timed_launch(K_W2, qbytes(ly.w2), [&] {
+                return launch_mm_mfma(ly.w2, xh, xda, n, x, E, 0, EPI_RESID, nullptr, stream);
+            });
+        }
+        if (!model.has_head) return;
+        if (last_only || !mm_mfma_supported(model.output)) {
+            MvLaunch o;
+            o.w = model.output; o.x = x; o.g = model.norm; o.sp = sp_d; o.y = logits_d;
+            o.tok0 = last_only ? n - 1 : 0;
+            o.n_tokens = last_only ? 1 : n;
+            timed_launch(K_LMHEAD, qbytes(model.output), [&] { return mv_launch(o, PRO_NORM, EPI_STORE, stream); });
+        } else {
+            timed_launch(K_LMHEAD, 0, [&] { return launch_act_f16(x, model.norm, n, E, xh, xda, stream); });
+            timed_launch(K_LMHEAD, qbytes(model.output), [&] {
+                return launch_mm_mfma(model.output, xh, xda, n, logits_d, (int) hp.n_vocab, 0, EPI_STORE, nullptr,
+                                      stream);
+            });
+        }
+        if (want_embedding)
+            LVK_HIP(launch_rmsnorm_rows(x + (size_t) (n - 1) * E, model.norm, E, 1, emb_d, stream));
+        return;
+    }
     // single-token FFN: W1|W3 hands silu(w1 x)*(w3 x) to W2 in f32, W2 quantizes it
     const bool ffn_f32 = n == 1 && model.qtype == Q4_0 && matvec_cu_supported(E) && matvec_cu_supported(F);
     if (model.has_embed)

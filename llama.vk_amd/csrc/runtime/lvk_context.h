@@ -47,6 +47,14 @@ struct Context {
     StepParams * sp_h = nullptr; // pinned
     int * tok_h = nullptr;       // pinned
 
+    // prompt (N > 1) path: MFMA matmuls with exact block dots (default) or the
+    // bit-faithful VALU kernels (prompt_exact; env LVK_PROMPT_EXACT=1)
+    bool prompt_exact = false;
+    uint16_t * xh = nullptr;     // [Cpad][max(E,F)] f16 quantized activations (MFMA operand)
+    float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales
+    float * qkv32 = nullptr;     // [C][3E] Q|K|V rows before RoPE
+    float * uf = nullptr;        // [C][F] silu(w1 x) * (w3 x)
+
     // decode graph (N = 1, last-token logits)
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
@@ -77,6 +85,7 @@ struct Context {
     // stage boundary: copy the residual stream x [n][E] to (to_ctx) or from the context
     void x_copy(void * buf, int n, bool to_ctx, bool on_device);
     void enqueue_forward(int n, bool last_only);
+    bool use_mfma(int n) const;
     void build_graph();
     void kv_get();
     void kv_set(const uint8_t * src, size_t n);

@@ -134,6 +134,30 @@ int lvk_mul_mat_q_norm(int type, const void * w, int m, int k, const float * g, 
     catch (const lvk::Error & e) { return fail(__func__, e.msg); }
 }
 
+int lvk_mul_mat_q_mfma(int type, const void * w, int m, int k, const float * g, const float * x, int n, float * y) {
+    try {
+        if (type != lvk::Q4_0) return fail(__func__, "Q4_0 only");
+        if (m % 128 || k % 256 || n < 1) return fail(__func__, "need m % 128 == 0, k % 256 == 0, n >= 1");
+        Dev dv;
+        const size_t nb = (size_t) k / 32;
+        void * wd = dv.up((const uint8_t *) w, (size_t) m * nb * 20);
+        lvk::QMatrix q;
+        q.qtype = type; q.M = m; q.K = k;
+        q.nib = (const uint4 *) dv.get(lvk::qimage_nib_bytes(m, k));
+        q.scl = dv.get(lvk::qimage_scl_bytes(m, k, type));
+        LVK_HIP(lvk::launch_repack(wd, type, m, k, (uint4 *) q.nib, (void *) q.scl, nullptr));
+        float * xd = dv.up(x, (size_t) n * k);
+        const float * gd = g ? dv.up(g, (size_t) k) : nullptr;
+        uint16_t * xh = (uint16_t *) dv.get((size_t) n * k * 2);
+        float * da = (float *) dv.get((size_t) n * nb * 4);
+        float * yd = (float *) dv.get((size_t) n * m * 4);
+        LVK_HIP(lvk::launch_act_f16(xd, gd, n, k, xh, da, nullptr));
+        LVK_HIP(lvk::launch_mm_mfma(q, xh, da, n, yd, m, 0, lvk::EPI_STORE, nullptr, nullptr));
+        LVK_HIP(hipMemcpy(y, yd, (size_t) n * m * 4, hipMemcpyDeviceToHost));
+        return 0;
+    } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
 int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
                          int n_ctx, int n_past, int n, float * out, float * scores_out);
 int lvk_attention(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head, int n_ctx,
@@ -235,5 +259,7 @@ int lvk_get_profile(struct llama_context * ctx, double * ms, long * launches, do
 }
 size_t lvk_weight_bytes(struct llama_context * ctx) { return ctx->c.model.weight_bytes; }
 void lvk_set_graph(struct llama_context * ctx, int on) { ctx->c.use_graph = on != 0; }
+
+void lvk_set_prompt_exact(struct llama_context * ctx, int on) { ctx->c.prompt_exact = on != 0; }
 
 }  // extern "C"

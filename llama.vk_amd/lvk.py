@@ -84,6 +84,7 @@ _sig("lvk_set_device", C.c_int, [C.c_int])
 _sig("lvk_quantize_rows", C.c_int, [C.c_int, f32p, C.c_int, C.c_int, u8p])
 _sig("lvk_mul_mat_q", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, f32p, C.c_int, f32p])
 _sig("lvk_mul_mat_q_norm", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, f32p, f32p, C.c_int, f32p])
+_sig("lvk_mul_mat_q_mfma", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, C.c_void_p, f32p, C.c_int, f32p])
 _sig("lvk_attention", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p])
 _sig("lvk_attention_scores", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p, f32p])
 _sig("lvk_rms_norm_mul", C.c_int, [f32p, f32p, C.c_int, C.c_int, f32p])
@@ -94,6 +95,7 @@ _sig("lvk_get_profile", C.c_int, [C.c_void_p, f64p, i64p, f64p, C.c_int])
 _sig("lvk_reset_profile", None, [C.c_void_p])
 _sig("lvk_weight_bytes", C.c_size_t, [C.c_void_p])
 _sig("lvk_set_graph", None, [C.c_void_p, C.c_int])
+_sig("lvk_set_prompt_exact", None, [C.c_void_p, C.c_int])
 _sig("lvk_init_stage", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, C.c_int])
 _sig("lvk_stage_eval", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_get_x", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
@@ -200,6 +202,10 @@ class Llama:
     def set_graph(self, on):
         lib.lvk_set_graph(self.ctx, int(on))
 
+    def set_prompt_exact(self, on):
+        """prompt batches on the bit-faithful VALU path (True) or the MFMA path (False, default)"""
+        lib.lvk_set_prompt_exact(self.ctx, int(on))
+
     def reset_profile(self):
         lib.lvk_reset_profile(self.ctx)
 
@@ -258,6 +264,20 @@ def mul_mat_q_norm(qtype, w_rows, m, k, g, x):
     y = np.zeros(n * m, np.float32)
     _check(lib.lvk_mul_mat_q_norm(qtype, np.ascontiguousarray(w_rows, np.uint8).ravel(), m, k,
                                   np.ascontiguousarray(g, np.float32), x, n, y), "lvk_mul_mat_q_norm")
+    return y.reshape(n, m)
+
+
+def mul_mat_q_mfma(qtype, w_rows, m, k, x, g=None):
+    """the MFMA prompt matmul (lvk_mul_mat_q_mfma); g: optional RMSNorm weight"""
+    x = np.ascontiguousarray(x, np.float32)
+    n = x.shape[0]
+    y = np.zeros(n * m, np.float32)
+    gp = None
+    if g is not None:
+        g = np.ascontiguousarray(g, np.float32)
+        gp = g.ctypes.data_as(C.c_void_p)
+    _check(lib.lvk_mul_mat_q_mfma(qtype, np.ascontiguousarray(w_rows, np.uint8).ravel(), m, k, gp, x, n, y),
+           "lvk_mul_mat_q_mfma")
     return y.reshape(n, m)
 
 

@@ -224,6 +224,26 @@ static float hsum8(const float a[8]) {
     return (r0 + r2) + (r1 + r3);
 }
 
+/* Test-only model of the MFMA prompt matmul's order (see lvk_oracle.h): the
+ * block dot of ggml_vec_dot_q4_0 (ggml.c:1950-2026) as one exact integer per
+ * block, one fp32 chain over the blocks. */
+float orc_vec_dot_q4_0_blockorder(int n, const void* vx, const void* vy) {
+    const blk_q4_0* x = (const blk_q4_0*) vx;
+    const blk_q4_0* y = (const blk_q4_0*) vy;
+    float acc = 0.0f;
+    for (int i = 0; i < n / QK; ++i) {
+        int p = 0;
+        for (int b = 0; b < QK / 2; ++b) {
+            const int xl = (x[i].qs[b] & 15) - 8, xh = (x[i].qs[b] >> 4) - 8;
+            const int yl = (y[i].qs[b] & 15) - 8, yh = (y[i].qs[b] >> 4) - 8;
+            p += xl * yl + xh * yh;
+        }
+        const float s = x[i].d * y[i].d;
+        acc = fmaf(s, (float) p, acc);
+    }
+    return acc;
+}
+
 /* ggml_vec_dot_q4_0 AVX2 (ggml.c:1950-2026).  Lane j of the 8-float acc
  * receives the block's elements 4j..4j+3 (madd of low-nibble and high-nibble
  * int16 vectors, ggml.c:2006-2010). */

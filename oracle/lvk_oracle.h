@@ -41,6 +41,11 @@ void orc_dequantize_row_q4_1(const void* x, float* y, int k);
 /* block dots, AVX2 accumulation order (ggml.c:1950-2026, 2188-2258) */
 float orc_vec_dot_q4_0(int n, const void* x, const void* y);
 float orc_vec_dot_q4_1(int n, const void* x, const void* y);
+/* NOT a reference function: the accumulation order of llama.vk_amd's MFMA
+ * prompt matmul (mm_mfma.hip) -- exact per-block integer dot I_b, then
+ * acc = fmaf(dx*dy, (float) I_b, acc) in block order -- so tests can pin that
+ * kernel bit-for-bit (its integer dots included) */
+float orc_vec_dot_q4_0_blockorder(int n, const void* x, const void* y);
 /* f16 dot (ggml.c:1781-1815, AVX F16 macros 1318-1416) */
 float orc_vec_dot_f16(int n, const uint16_t* x, const uint16_t* y);
 

@@ -43,7 +43,7 @@ class Oracle:
             _sig(L, n, None, [f32p, u8p, C.c_int])
         for n in ("orc_dequantize_row_q4_0", "orc_dequantize_row_q4_1"):
             _sig(L, n, None, [u8p, f32p, C.c_int])
-        for n in ("orc_vec_dot_q4_0", "orc_vec_dot_q4_1"):
+        for n in ("orc_vec_dot_q4_0", "orc_vec_dot_q4_1", "orc_vec_dot_q4_0_blockorder"):
             _sig(L, n, C.c_float, [C.c_int, u8p, u8p])
         _sig(L, "orc_vec_dot_f16", C.c_float, [C.c_int, u16p, u16p])
         _sig(L, "orc_rms_norm", None, [f32p, C.c_int, C.c_int, f32p])

@@ -29,6 +29,7 @@ def test_tiny_matches_reference_golden(lvk, tiny_models, name, graph):
     g = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
     m = lvk.Llama(tiny_models[name], n_ctx=512)
     m.set_graph(graph)
+    m.set_prompt_exact(True)     # bit-exact prompt chunks (the MFMA path: test_mfma_prompt_*)
     n_past, off = 0, 0
     for step, n in enumerate(g["chunks"]):
         lg = m.eval(g["tokens"][off:off + n], n_past)
@@ -41,6 +42,7 @@ def test_tiny_matches_reference_golden(lvk, tiny_models, name, graph):
 def test_tiny_q4_0_long_decode_vs_oracle(lvk, oracle, tiny_models):
     path = tiny_models["tiny_q4_0"]
     m = lvk.Llama(path, n_ctx=256)
+    m.set_prompt_exact(True)
     om = oracle.model(path, 256)
     toks = np.array([1, 450, 4996, 17354, 1701, 29916], np.int32)
     a = m.eval(toks, 0)
@@ -61,6 +63,7 @@ def test_tiny_q4_0_long_decode_vs_oracle(lvk, oracle, tiny_models):
 def test_logits_all_and_embeddings(lvk, oracle, tiny_models):
     path = tiny_models["tiny_q4_0"]
     m = lvk.Llama(path, n_ctx=128, logits_all=True, embedding=True)
+    m.set_prompt_exact(True)
     om = oracle.model(path, 128)
     toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 40)], np.int32)
     a = m.eval(toks, 0)
@@ -76,11 +79,13 @@ def test_logits_all_and_embeddings(lvk, oracle, tiny_models):
 def test_kv_cache_roundtrip(lvk, tiny_models):
     path = tiny_models["tiny_q4_0"]
     m = lvk.Llama(path, n_ctx=128)
+    m.set_prompt_exact(True)
     toks = np.arange(1, 20, dtype=np.int32)
     m.eval(toks, 0)
     kv = m.kv_cache()
     a = m.eval([42], 19)
     m2 = lvk.Llama(path, n_ctx=128)
+    m2.set_prompt_exact(True)
     m2.set_kv_cache(kv, 19)
     b = m2.eval([42], 19)
     assert np.array_equal(bits(a), bits(b))
@@ -104,6 +109,7 @@ def test_7b_shaped_decode_vs_oracle(lvk, oracle, model_dir):
     from oracle_lib import gen_model
     path = gen_model(os.path.join(model_dir, "w4096_l2.bin"), n_embd=4096, n_head=32, n_layer=2, ftype=2, seed=7)
     m = lvk.Llama(path, n_ctx=512)
+    m.set_prompt_exact(True)
     om = oracle.model(path, 512)
     toks = np.array([1, 450, 4996, 17354, 1701, 29916, 338, 263], np.int32)
     a = m.eval(toks, 0)
@@ -138,5 +144,59 @@ def test_13b_shaped_q4_1_decode_vs_oracle(lvk, oracle, model_dir):
         assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past
         n_past += 1
         tok = int(np.argmax(a[-1]))
+    m.close()
+    om.close()
+
+
+# ---------------------------------------------------------------------------
+# MFMA prompt path (default for N > 1): bit-exact like the VALU path.
+# ---------------------------------------------------------------------------
+def test_mfma_prompt_tiny_logits_all_vs_oracle(lvk, oracle, tiny_models):
+    """every position of a 100-token prompt (logits_all) through the MFMA matmuls"""
+    path = tiny_models["tiny_q4_0"]
+    m = lvk.Llama(path, n_ctx=256, logits_all=True)
+    om = oracle.model(path, 256)
+    toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 100)], np.int32)
+    a = m.eval(toks, 0)
+    b = om.eval(toks, 0, logits_all=True)
+    assert a.shape == b.shape == (100, m.n_vocab)
+    assert np.array_equal(bits(a), bits(b))
+    m.close()
+    om.close()
+
+
+@pytest.mark.parametrize("name", ["tiny_q4_0"])
+def test_mfma_prompt_chunks_match_reference_golden(lvk, tiny_models, name):
+    """the reference's chunking (prompt batches 16, 8, 24, then decode) with MFMA prompt batches,
+    against the logits the reference build produced"""
+    g = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+    m = lvk.Llama(tiny_models[name], n_ctx=512)
+    n_past, off = 0, 0
+    for step, n in enumerate(g["chunks"]):
+        lg = m.eval(g["tokens"][off:off + n], n_past)
+        assert np.array_equal(bits(lg[-1]), bits(g["logits"][step])), "step %d (n=%d, n_past=%d)" % (step, n, n_past)
+        n_past += n
+        off += n
+    m.close()
+
+
+def test_mfma_prompt_7b_shaped_vs_oracle(lvk, oracle, model_dir):
+    """LLaMA-7B layer shapes (K = 4096 / 11008, 32 heads), 2 layers, a 200-token prompt (ragged
+    last token tile) through the MFMA matmuls, then decode on the KV cache it wrote"""
+    from oracle_lib import gen_model
+    path = gen_model(os.path.join(model_dir, "w4096_l2.bin"), n_embd=4096, n_head=32, n_layer=2, ftype=2, seed=7)
+    m = lvk.Llama(path, n_ctx=512)
+    om = oracle.model(path, 512)
+    toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 200)], np.int32)
+    a = m.eval(toks, 0)
+    b = om.eval(toks, 0)
+    assert np.array_equal(bits(a), bits(b))
+    n_past, tok = len(toks), int(np.argmax(b[-1]))
+    for _ in range(4):
+        a = m.eval([tok], n_past)
+        b = om.eval([tok], n_past)
+        assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past
+        n_past += 1
+        tok = int(np.argmax(b[-1]))
     m.close()
     om.close()

@@ -128,3 +128,26 @@ def test_rms_norm_mul(lvk, oracle):
     oracle.lib.orc_rms_norm(x, 4096, 4, want)
     want = (g[None, :] * want).astype(np.float32)
     assert np.array_equal(bits(got), bits(want))
+
+
+# ---------------------------------------------------------------------------
+# MFMA prompt matmul (mm_mfma.hip): the matrix cores produce the per-chain
+# integer partials, the VALU runs the reference's fp32 chains -> bit-exact
+# against ggml_vec_dot_q4_0's AVX2 order, incl. the fused RMSNorm+quantize.
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("m,k,n,norm", [(128, 256, 2, False), (256, 4096, 64, True), (128, 4096, 70, False),
+                                        (128, 11008, 17, False), (384, 1024, 130, True), (128, 5120, 3, True)])
+def test_mul_mat_mfma_bit_exact(lvk, oracle, m, k, n, norm):
+    rng = np.random.default_rng(m + 3 * k + 11 * n)
+    wq = _weights(oracle, rng, m, k, 2)
+    x = (rng.standard_normal((n, k)) * 1.7).astype(np.float32)
+    x[0, :32] = 0.0                                   # an all-zero activation block (d = 0)
+    g = (1.0 + 0.1 * rng.standard_normal(k)).astype(np.float32) if norm else None
+    got = lvk.mul_mat_q_mfma(2, wq, m, k, x, g=g)
+    xin = x
+    if norm:
+        xn = np.zeros_like(x)
+        oracle.lib.orc_rms_norm(x, k, n, xn)
+        xin = (g[None, :] * xn).astype(np.float32)
+    want = _oracle_mm(oracle, wq, [oracle.quantize(r, 2) for r in xin], k, 2)
+    assert np.array_equal(bits(got), bits(want))

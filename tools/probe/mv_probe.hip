@@ -31,6 +31,20 @@ __global__ void k_fill_f16(uint16_t * p, size_t n, uint32_t seed) {
         p[i] = (uint16_t) (0x2C00 + (h & 0x3FF)) | (uint16_t) ((h >> 16) & 0x8000);
     }
 }
+// side-stream prefetch: pulls a byte range through the memory hierarchy (MALL allocation)
+template <int U>
+__global__ void k_prefetch(const uint4 * __restrict__ p, size_t n, unsigned * out) {
+    unsigned acc = 0;
+    const size_t stride = (size_t) gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t) blockDim.x + threadIdx.x; i < n; i += stride * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) { size_t j = i + u * stride; j = j < n ? j : n - 1; v[u] = p[j]; }
+#pragma unroll
+        for (int u = 0; u < U; u++) acc ^= v[u].x + v[u].y;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
 static void fill_u32(void * p, size_t bytes, uint32_t seed) { hipLaunchKernelGGL(k_fill_u32, dim3(1024), dim3(256), 0, 0, (uint32_t *) p, bytes / 4, seed); }
 static void fill_f32(void * p, size_t n, float lo, float hi, uint32_t seed) { hipLaunchKernelGGL(k_fill_f32, dim3(1024), dim3(256), 0, 0, (float *) p, n, lo, hi, seed); }
 static void * dalloc(size_t b) { void * p; CK(hipMalloc(&p, b + 4096)); return p; }
@@ -49,7 +63,9 @@ int main(int argc, char ** argv) {
     const int n_past = argc > 1 ? atoi(argv[1]) : 256;
     struct Lay { QMatrix qkv, wo, w13, w2; };
     std::vector<Lay> ly(L);
+    const bool hot = getenv("LVK_PROBE_HOT") != nullptr;   // every layer aliases layer 0 (MALL-resident)
     for (int l = 0; l < L; l++) {
+        if (hot && l > 0) { ly[l] = ly[0]; continue; }
         ly[l].qkv = mkmat(3 * E, E, 100 * l + 1); ly[l].wo = mkmat(E, E, 100 * l + 2);
         ly[l].w13 = mkmat(2 * F, E, 100 * l + 3); ly[l].w2 = mkmat(E, F, 100 * l + 4);
     }
@@ -109,8 +125,30 @@ int main(int argc, char ** argv) {
     const double bytes[6] = {3.0 * E * E / 32 * 20, 0, 1.0 * E * E / 32 * 20, 2.0 * F * E / 32 * 20, 1.0 * F * E / 32 * 20, 1.0 * V * E / 32 * 20};
     // x is re-normalised by every RESID add; keep it bounded by re-filling before each graph (not timed)
     hipGraph_t gr; hipGraphExec_t ge;
+    const int pf = getenv("LVK_PROBE_PF") ? atoi(getenv("LVK_PROBE_PF")) : 0;   // prefetch WG count
+    const int pft = getenv("LVK_PROBE_PFT") ? atoi(getenv("LVK_PROBE_PFT")) : 128;
+    const int pfk = getenv("LVK_PROBE_PFK") ? atoi(getenv("LVK_PROBE_PFK")) : 0;  // fork after op k of layer l
+    hipStream_t s2; CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    unsigned * pfo = (unsigned *) dalloc(64);
+    std::vector<hipEvent_t> evs(L + 1);
+    for (auto & ev : evs) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    auto prefetch = [&](const QMatrix & q) {
+        size_t nb = qimage_nib_bytes(q.M, q.K) / 16, sb = qimage_scl_bytes(q.M, q.K) / 16;
+        hipLaunchKernelGGL(k_prefetch<8>, dim3(pf), dim3(pft), 0, s2, q.nib, nb, pfo);
+        hipLaunchKernelGGL(k_prefetch<8>, dim3(pf), dim3(pft), 0, s2, (const uint4 *) q.scl, sb, pfo);
+    };
     CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
-    for (int l = 0; l < L; l++) for (int k = 0; k < 5; k++) op(k, l);
+    for (int l = 0; l < L; l++) {
+        for (int k = 0; k < 5; k++) {
+            op(k, l);
+            if (pf && k == pfk && l + 1 < L) {
+                CK(hipEventRecord(evs[l], s));
+                CK(hipStreamWaitEvent(s2, evs[l], 0));
+                prefetch(ly[l + 1].qkv); prefetch(ly[l + 1].wo); prefetch(ly[l + 1].w13); prefetch(ly[l + 1].w2);
+            }
+        }
+    }
+    if (pf) { CK(hipEventRecord(evs[L], s2)); CK(hipStreamWaitEvent(s, evs[L], 0)); }
     op(5, 0);
     CK(hipStreamEndCapture(s, &gr));
     CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
