@@ -141,17 +141,20 @@ inline size_t qimage_scl_bytes(int M, int K, int qtype = Q4_0) {
     return (size_t) M * ((K / 32 + 31) / 32) * 128 * (qtype == Q4_1 ? 2 : 1);
 }
 
-// prompt-eval (N > 1) Q4_0 matmul on the MFMA cores (mm_mfma.hip): exact
-// per-block integer dots, fp32 block scaling in block order.  Input: f16
-// activations xh [N][K] (values q-8 in the kernel's k order) + da [N][K/32]
-// from launch_act_f16 / launch_actq_to_f16.  epi: EPI_STORE, EPI_RESID
-// (y += W x), EPI_SWIGLU_F32 (fused W1|W3 image -> u = silu(w1 x) * (w3 x)).
+// prompt-eval (N > 1) Q4_0 matmul on the MFMA cores (mm_mfma.hip), bit-exact
+// like launch_matvec: the matrix cores produce the per-chain integer partials,
+// the VALU runs the reference fp32 chains.  Input: the masked B fragment image
+// xm (mm_act_bytes(N, K) bytes, ZEROED once at allocation: only the active
+// slots are ever written) + da [N][K/32], from launch_act_f16 /
+// launch_actq_to_f16.  epi: EPI_STORE, EPI_RESID (y += W x), EPI_SWIGLU_F32
+// (fused W1|W3 image -> u = silu(w1 x) * (w3 x)).
 bool mm_mfma_supported(const QMatrix & w);
-hipError_t launch_mm_mfma(const QMatrix & w, const uint16_t * xh, const float * da, int N, float * y, int ldy,
+size_t mm_act_bytes(int N, int K);
+hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, int N, float * y, int ldy,
                           int out_tok0, int epi, const uint16_t * silu_tab, hipStream_t s);
-// x[N][K] (rms_norm * g when g != nullptr) -> quantize_row_q4_0 -> xh, da
-hipError_t launch_act_f16(const float * x, const float * g, int N, int K, uint16_t * xh, float * da, hipStream_t s);
-hipError_t launch_actq_to_f16(const ActQ & q, int N, int K, uint16_t * xh, float * da, hipStream_t s);
+// x[N][K] (rms_norm * g when g != nullptr) -> quantize_row_q4_0 -> xm, da
+hipError_t launch_act_f16(const float * x, const float * g, int N, int K, void * xm, float * da, hipStream_t s);
+hipError_t launch_actq_to_f16(const ActQ & q, int N, int K, void * xm, float * da, hipStream_t s);
 // RoPE + KV append of stored Q|K|V rows qkv [N][3E]
 hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 * rope, const StepParams * sp,
                           int n_ctx, uint16_t * q16, uint16_t * kc, uint16_t * vc, hipStream_t s);

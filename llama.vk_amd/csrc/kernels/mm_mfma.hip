@@ -25,10 +25,14 @@
 //     2c+h, c = 0..3) of its row group, 4 x 16 B per 8 blocks; nibbles -> f16
 //     with the magic-exponent trick (0x6400|q = 1024+q, 0x4C00|q<<4 = 16+q/4)
 //     in the chain order e0 e2 e1 e3.
-//   B (activations): Q4_0-quantized tokens as f16 values q-8 [N][K] in the
-//     same per-chain order (launch_act_f16), staged per 4 blocks through LDS
-//     into the masked fragment image [block][c][jj][h][token] whose h != jj
-//     slots stay zero, so every lane reads its fragment with one ds_read_b64.
+//   B (activations): Q4_0-quantized tokens as f16 values q-8, written by the
+//     activation quantizer straight into the masked fragment image
+//       xm[token tile][block][c][64 lanes] x 8 B
+//     (lane (h, jj, n): chain 2c+h of token n when h == jj, else zero), so a
+//     wave loads each fragment with one coalesced global_load_dwordx2 -- no
+//     LDS staging and no barrier per K step; 4 blocks are kept in flight.
+//   Scales: dw (octet image) and da staged per 32-block chunk in LDS (one
+//     barrier per chunk).
 // Workgroup = 4 waves, tile 128 rows x 16 tokens (wave w: rows 32w..32w+31,
 // all 8 chains: 64 accumulator registers); workgroups are mapped so the 8
 // XCDs each sweep contiguous row tiles with the token tiles innermost (the
@@ -46,28 +50,31 @@ typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
 constexpr int TM = 128;     // rows per workgroup
-constexpr int TN = 16;      // tokens per workgroup
+constexpr int TN = 16;      // tokens per workgroup (one token tile)
 constexpr int NT = 256;     // threads (4 waves)
-constexpr int SBK = 4;      // blocks per LDS stage
+// LVK_MM_EXP (dev probe builds only, tools/probe), bit flags: 1 no fp32 chains, 2 no MFMA, 4 no B loads,
+// 8 no A loads, 16 no scale LDS reads
+#ifndef LVK_MM_EXP
+#define LVK_MM_EXP 0
+#endif
+#ifndef LVK_MM_PD
+#define LVK_MM_PD 4
+#endif
+constexpr int PD = LVK_MM_PD;   // B blocks in flight per wave (ring size divides 8)
 
-// masked B image: per (block, c) 4 slots (jj, h) of 16 tokens x 8 B, slot stride
-// 192 B (48 dwords: the two slots a ds_read_b64 half-wave touches fall in
-// disjoint bank halves)
-constexpr int SLOT = 192;
-constexpr int BC_BYTES = 4 * SLOT;                  // one (block, c)
-constexpr int LDS_B = SBK * 4 * BC_BYTES;           // 12 KiB per stage buffer
-constexpr int LDS_DW = 32 * TM * 4;                 // 16 KiB: [block of chunk][row]
-constexpr int LDS_DA = 32 * TN * 4;                 // 2 KiB:  [block of chunk][token]
-constexpr int OFF_B0 = 0, OFF_B1 = LDS_B;
-constexpr int OFF_DW0 = 2 * LDS_B, OFF_DW1 = OFF_DW0 + LDS_DW;
-constexpr int OFF_DA0 = OFF_DW1 + LDS_DW, OFF_DA1 = OFF_DA0 + LDS_DA;
-constexpr int LDS_TOTAL = OFF_DA1 + LDS_DA;         // 60 KiB: two workgroups per CU
+constexpr int DWS = TM + 8;                         // padded row stride of the dw image (conflict-free stores)
+constexpr int DAS = TN + 1;                         // padded stride of the da image
+constexpr int LDS_DW = 32 * DWS * 4;                // [block of chunk][row]
+constexpr int LDS_DA = (32 * DAS * 4 + 15) / 16 * 16;   // [block of chunk][token]
+constexpr int OFF_DW0 = 0, OFF_DW1 = LDS_DW;
+constexpr int OFF_DA0 = 2 * LDS_DW, OFF_DA1 = OFF_DA0 + LDS_DA;
+constexpr int LDS_TOTAL = OFF_DA1 + LDS_DA;         // ~37 KiB
 
 struct MmParams {
     const uint4 * nib;
     const float4 * scl;
     int M, K, nb, NC;
-    const uint16_t * xh;     // [N][K] f16 (per-chain order e0 e2 e1 e3)
+    const uint2 * xm;        // masked B fragment image [ntt][nb][4][64]
     const float * da;        // [N][nb]
     int N;                   // tokens
     int ntt;                 // token tiles
@@ -98,6 +105,14 @@ __device__ __forceinline__ half4_t unpack_chain(uint32_t X, uint32_t sel) {
     return r;
 }
 
+__device__ __forceinline__ f32x16_t fake_mfma(half4_t a, half4_t b) {   // LVK_MM_EXP & 2 only
+    f32x16_t r;
+    const float v = (float) a[0] + (float) b[1];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = v;
+    return r;
+}
+
 template <int EPI>
 __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -107,41 +122,20 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
     // XCD-aware tile order: workgroup b runs on XCD b % 8; give each XCD a
     // contiguous range of (row tile, token tile) with token tiles innermost
     const int nwg = gridDim.x;
-    const int b = blockIdx.x;
+    const int bid = blockIdx.x;
     const int full = nwg & ~7;
-    const int L = b < full ? (b & 7) * (full >> 3) + (b >> 3) : b;
+    const int L = bid < full ? (bid & 7) * (full >> 3) + (bid >> 3) : bid;
+    const int tt = L % P.ntt;
     const int m0 = (L / P.ntt) * TM;
-    const int n0 = (L % P.ntt) * TN;
-    const int K = P.K, nb = P.nb, NC = P.NC;
-    const int S = nb / SBK;                    // stages (even: nb % 8 == 0)
+    const int n0 = tt * TN;
+    const int nb = P.nb, NC = P.NC;
     const int G0 = m0 / 8;
+    const int U = nb / 8;                      // sub-chunks of 8 blocks
 
-    // zero the masked (h != jj) slots of both B buffers once
-    for (int i = tid; i < 2 * SBK * 4 * 2 * (TN * 8 / 16); i += NT) {
-        const int per = TN * 8 / 16;                      // uint4 per slot
-        const int q = i % per, rest = i / per;
-        const int which = rest & 1, bc = rest >> 1;       // which: slot 1 or 2
-        ((uint4 *) (smem + (size_t) bc * BC_BYTES + (which ? 2 : 1) * SLOT))[q] = make_uint4(0, 0, 0, 0);
-    }
-
-    // ---- staging registers (global -> LDS) ----
-    uint4 rb;             // B: 16 B per thread per stage
-    float rda[2];         // da: chunk boundary
-    float4 rdw[4];        // dw: chunk boundary
-    auto load_b = [&](int s) {
-        const int n = tid >> 4, u = tid & 15;              // token, uint4 of its 256 B stage slice
-        const int tok = min(n0 + n, P.N - 1);
-        rb = *(const uint4 *) (P.xh + (size_t) tok * K + (size_t) s * (SBK * 32) + u * 8);
-    };
-    auto store_b = [&](int s) {
-        uint8_t * bl = smem + ((s & 1) ? OFF_B1 : OFF_B0);
-        const int n = tid >> 4, u = tid & 15;
-        const int jb = u >> 2, c = u & 3;                 // chains 2c (first 8 B), 2c+1
-        uint8_t * bc = bl + (jb * 4 + c) * BC_BYTES;
-        *(uint2 *) (bc + 0 * SLOT + n * 8) = make_uint2(rb.x, rb.y);    // (jj 0, h 0)
-        *(uint2 *) (bc + 3 * SLOT + n * 8) = make_uint2(rb.z, rb.w);    // (jj 1, h 1)
-    };
-    auto load_scales = [&](int c) {        // chunk c: 32 blocks
+    // ---- scales: chunk c (32 blocks) staged into LDS buffer c & 1 ----
+    float rda[2];
+    float4 rdw[4];
+    auto load_scales = [&](int c) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int Li = i * NT + tid;
@@ -164,13 +158,13 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
             const int r = l >> 3, j = l & 7;
             const float v[4] = {rdw[i].x, rdw[i].y, rdw[i].z, rdw[i].w};
 #pragma unroll
-            for (int m = 0; m < 4; ++m) wl[(8 * m + j) * TM + 8 * G + r] = v[m];
+            for (int m = 0; m < 4; ++m) wl[(8 * m + j) * DWS + 8 * G + r] = v[m];
         }
         float * dl = (float *) (smem + ((c & 1) ? OFF_DA1 : OFF_DA0));
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int Li = i * NT + tid;
-            dl[(Li & 31) * TN + (Li >> 5)] = rda[i];
+            dl[(Li & 31) * DAS + (Li >> 5)] = rda[i];
         }
     };
 
@@ -181,7 +175,20 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
     auto load_a = [&](int u, uint4 (&A)[4]) {              // sub-chunk u = 8 blocks
         const uint4 * p = ap + (size_t) u * 64;            // (c*4 + sb) * 64 == u * 64
 #pragma unroll
-        for (int c = 0; c < 4; ++c) A[c] = ld_nt(p + 2 * c);
+        for (int c = 0; c < 4; ++c) {
+            if (LVK_MM_EXP & 8) A[c] = make_uint4(u, c, u ^ c, 7);
+            else A[c] = p[2 * c];
+        }
+    };
+    // ---- B operand: masked fragments of this token tile, 4 per block ----
+    const uint2 * bp = P.xm + (size_t) tt * nb * 256 + lane;
+    uint2 bq[PD][4];
+    auto load_bq = [&](int blk, uint2 (&q)[4]) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (LVK_MM_EXP & 4) q[c] = make_uint2(blk, c);
+            else q[c] = bp[(size_t) blk * 256 + c * 64];
+        }
     };
 
     f32x16_t acc[4];
@@ -190,86 +197,89 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[c][i] = 0.0f;
 
-    // B fragment lane offset: slot (jj, h), token lane&15
-    const int jj = (lane >> 4) & 1;
-    const int boff = (jj * 2 + h) * SLOT + (lane & 15) * 8;
-
-    const int U = nb / 8;
-    uint4 Acur[4], Anext[4];
-    load_b(0);
-    load_scales(0);
-    load_a(0, Acur);
-    store_b(0);
-    store_scales(0);
-    __syncthreads();
-
-    // one stage = 4 blocks; ko selects the A dwords (0: blocks 0-3 of the sub-chunk, 2: blocks 4-7)
-    auto compute_stage = [&](int s, int ko, const uint32_t (&X)[4][4]) {
-        const uint8_t * bl = smem + ((s & 1) ? OFF_B1 : OFF_B0);
-        const int ch = s >> 3;                              // chunk
-        const float * wl = (const float *) (smem + ((ch & 1) ? OFF_DW1 : OFF_DW0));
-        const float * dl = (const float *) (smem + ((ch & 1) ? OFF_DA1 : OFF_DA0));
+    uint32_t X[4][4];                                     // signed octet nibbles -> unsigned q
+    auto make_x = [&](const uint4 (&A)[4]) {
 #pragma unroll
-        for (int jb = 0; jb < SBK; ++jb) {
-            const int jc = (s & 7) * SBK + jb;              // block within the chunk
-            const uint32_t sel = (jb & 1) ? 0x0C030C02u : 0x0C010C00u;
-            half4_t bf[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                bf[c] = __builtin_bit_cast(half4_t, *(const uint2 *) (bl + (jb * 4 + c) * BC_BYTES + boff));
-            // block order pinned: nothing of this block is hoisted above the previous block's FMAs
-#pragma unroll
-            for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(bf[c]));
-            // s = dw * da for this lane's 16 rows (ggml.c:1968)
-            const float dav = dl[jc * TN + (lane & 15)];
-            float sc[16];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 d4 = *(const float4 *) (wl + jc * TM + 32 * w + 8 * q + 4 * h);
-                sc[4 * q + 0] = d4.x * dav; sc[4 * q + 1] = d4.y * dav;
-                sc[4 * q + 2] = d4.z * dav; sc[4 * q + 3] = d4.w * dav;
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const half4_t af = unpack_chain(X[c][ko + (jb >> 1)], sel);
-                const f32x16_t Pc = __builtin_amdgcn_mfma_f32_32x32x8f16(af, bf[c], (f32x16_t){}, 0, 0, 0);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[c][i] = __builtin_fmaf(sc[i], Pc[i], acc[c][i]);  // ggml.c:2013
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(acc[c]));
+        for (int c = 0; c < 4; ++c) {
+            X[c][0] = A[c].x ^ 0x88888888u; X[c][1] = A[c].y ^ 0x88888888u;
+            X[c][2] = A[c].z ^ 0x88888888u; X[c][3] = A[c].w ^ 0x88888888u;
         }
     };
 
+    uint4 Anext[4];
+    load_scales(0);
+    load_a(0, Anext);
+#pragma unroll
+    for (int d = 0; d < PD; ++d) load_bq(min(d, nb - 1), bq[d]);
+    store_scales(0);
+    make_x(Anext);
+    __syncthreads();
+
     for (int u = 0; u < U; ++u) {
+        const int ch = u >> 2;
+        const bool chunk_last = (u & 3) == 3 || u == U - 1;
+        const bool scales_next = chunk_last && u + 1 < U;
         if (u + 1 < U) load_a(u + 1, Anext);
-        uint32_t X[4][4];                                   // signed octet nibbles -> unsigned q
+        if (scales_next) load_scales(ch + 1);
+        const float * wl = (const float *) (smem + ((ch & 1) ? OFF_DW1 : OFF_DW0));
+        const float * dl = (const float *) (smem + ((ch & 1) ? OFF_DA1 : OFF_DA0));
+        // this lane's dw (16 rows) and da for block jc of the chunk, read one block ahead
+        float4 d4[4];
+        float dav;
+        auto read_scales = [&](int jc) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            X[c][0] = Acur[c].x ^ 0x88888888u; X[c][1] = Acur[c].y ^ 0x88888888u;
-            X[c][2] = Acur[c].z ^ 0x88888888u; X[c][3] = Acur[c].w ^ 0x88888888u;
+            for (int q = 0; q < 4; ++q) {
+                if (LVK_MM_EXP & 16) d4[q] = make_float4(jc, q, 1.f, 2.f);
+                else d4[q] = *(const float4 *) (wl + jc * DWS + 32 * w + 8 * q + 4 * h);
+            }
+            dav = (LVK_MM_EXP & 16) ? 1.5f : dl[jc * DAS + (lane & 15)];
+        };
+        read_scales((u & 3) * 8);
+#pragma unroll
+        for (int jb = 0; jb < 8; ++jb) {
+            const int blk = 8 * u + jb;
+            const uint32_t sel = (jb & 1) ? 0x0C030C02u : 0x0C010C00u;
+            uint2 (&bf)[4] = bq[jb % PD];
+            // s = dw * da for this lane's 16 rows (ggml.c:1968)
+            float sc[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                sc[4 * q + 0] = d4[q].x * dav; sc[4 * q + 1] = d4[q].y * dav;
+                sc[4 * q + 2] = d4[q].z * dav; sc[4 * q + 3] = d4[q].w * dav;
+            }
+            if (jb + 1 < 8) read_scales((u & 3) * 8 + jb + 1);     // in flight during this block's chains
+            // software pipeline: the MFMA of chain pair c+1 is in flight while the VALU runs the
+            // chains of pair c (ggml.c:2013: acc_j = fmaf(d, P_j, acc_j))
+            f32x16_t Pc[2];
+#define LVK_MFMA(a, b) ((LVK_MM_EXP & 2) ? fake_mfma(a, b) : __builtin_amdgcn_mfma_f32_32x32x8f16(a, b, (f32x16_t){}, 0, 0, 0))
+            Pc[0] = LVK_MFMA(unpack_chain(X[0][jb >> 1], sel), __builtin_bit_cast(half4_t, bf[0]));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (c + 1 < 4)
+                    Pc[(c + 1) & 1] = LVK_MFMA(unpack_chain(X[c + 1][jb >> 1], sel), __builtin_bit_cast(half4_t, bf[c + 1]));
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (LVK_MM_EXP & 1) acc[c][i] += (i == 0 ? Pc[c & 1][0] + sc[0] : 0.0f);
+                    else acc[c][i] = __builtin_fmaf(sc[i], Pc[c & 1][i], acc[c][i]);
+                }
+            }
+            // refill this slot with block blk + PD (its MFMAs have read the old fragments)
+            load_bq(min(blk + PD, nb - 1), bf);
+            // block order pinned: unconstrained, hipcc hoists later blocks' MFMAs and spills
+#pragma unroll
+            for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(acc[c]));
         }
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const int s = 2 * u + half;
-            const bool more = s + 1 < S;
-            const bool chunk_next = more && ((s + 1) & 7) == 0;
-            if (more) load_b(s + 1);
-            if (chunk_next) load_scales((s + 1) >> 3);
-            compute_stage(s, 2 * half, X);
-            if (more) store_b(s + 1);
-            if (chunk_next) store_scales((s + 1) >> 3);
-            __syncthreads();
-        }
-        if (u + 1 < U) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) Acur[c] = Anext[c];
+        if (u + 1 < U) make_x(Anext);
+        if (scales_next) {
+            store_scales(ch + 1);
+            __syncthreads();            // chunk ch+1's scales visible; chunk ch-1's buffer free again
         }
     }
 
     // ---- AVX2 horizontal order (ggml.c:2019-2024): lane (h, n, jj) register set c holds chain 2c+jj;
     // r_j = a_j + a_{j+4} (same lane, sets c and c+2), (r0+r2) | (r1+r3) in lanes jj = 0 | 1, then across
     // the lane pair (xor 16)
+    const int jj = (lane >> 4) & 1;
     float res[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -325,7 +335,7 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
 // ---------------------------------------------------------------------------
 template <bool NORM>
 __global__ __launch_bounds__(256) void k_act_q40_f16(const float * __restrict__ x, const float * __restrict__ g,
-                                                     int K, uint16_t * __restrict__ xh, float * __restrict__ da) {
+                                                     int K, uint2 * __restrict__ xm, float * __restrict__ da) {
     __shared__ double red[4];
     __shared__ float s_scale;
     const int t = blockIdx.x;
@@ -389,37 +399,38 @@ __global__ __launch_bounds__(256) void k_act_q40_f16(const float * __restrict__ 
                 const int q = ((int) __builtin_rintf(v[e] * id) + 8) & 15;   // ggml.c:655-684
                 h[e] = __builtin_bit_cast(uint16_t, (_Float16) (float) (q - 8));
             }
-            uint4 o;   // k order e0 e2 e1 e3 e4 e6 e5 e7
-            o.x = h[0] | (uint32_t) h[2] << 16; o.y = h[1] | (uint32_t) h[3] << 16;
-            o.z = h[4] | (uint32_t) h[6] << 16; o.w = h[5] | (uint32_t) h[7] << 16;
-            *(uint4 *) (xh + (size_t) t * K + u * 8) = o;
+            // masked fragment image: chain 2c -> lane n (h = jj = 0), chain 2c+1 -> lane 48 + n (h = jj = 1),
+            // each in the order e0 e2 e1 e3
+            const int nb = K / 32, c = u & 3;
+            uint2 * fr = xm + ((size_t) ((t >> 4) * nb + (u >> 2)) * 4 + c) * 64 + (t & 15);
+            fr[0] = make_uint2(h[0] | (uint32_t) h[2] << 16, h[1] | (uint32_t) h[3] << 16);
+            fr[48] = make_uint2(h[4] | (uint32_t) h[6] << 16, h[5] | (uint32_t) h[7] << 16);
             if ((u & 3) == 0) da[(size_t) t * (K / 32) + (u >> 2)] = d;
         }
     }
 }
 
-// pre-quantized Q4_0 blocks (ActQ: d + reference nibble qs) -> f16 + da
-__global__ void k_actq_to_f16(ActQ q, int N, int K, uint16_t * __restrict__ xh, float * __restrict__ da) {
+// pre-quantized Q4_0 blocks (ActQ: d + reference nibble qs) -> masked fragment image + da
+__global__ void k_actq_to_f16(ActQ q, int N, int K, uint2 * __restrict__ xm, float * __restrict__ da) {
     const int nb = K / 32;
     const long idx = (long) blockIdx.x * blockDim.x + threadIdx.x;   // (token, block, group of 8)
     if (idx >= (long) N * nb * 4) return;
-    const int gq = (int) (idx & 3);
+    const int c = (int) (idx & 3);
     const long tb = idx >> 2;
     const uint4 qs = q.qs[tb];
     const uint32_t wd[4] = {qs.x, qs.y, qs.z, qs.w};
-    const uint32_t word = wd[gq];              // elements 8gq..8gq+7: element 2k = byte k low nibble
+    const uint32_t word = wd[c];               // elements 8c..8c+7: element 2k = byte k low nibble
     uint16_t h[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const int qv = (int) ((word >> (4 * e)) & 15u);
         h[e] = __builtin_bit_cast(uint16_t, (_Float16) (float) (qv - 8));
     }
-    uint4 o;
-    o.x = h[0] | (uint32_t) h[2] << 16; o.y = h[1] | (uint32_t) h[3] << 16;
-    o.z = h[4] | (uint32_t) h[6] << 16; o.w = h[5] | (uint32_t) h[7] << 16;
     const long t = tb / nb, b = tb % nb;
-    *(uint4 *) (xh + (size_t) t * K + b * 32 + gq * 8) = o;
-    if (gq == 0) da[tb] = q.d[tb];
+    uint2 * fr = xm + ((size_t) ((t >> 4) * nb + b) * 4 + c) * 64 + (t & 15);
+    fr[0] = make_uint2(h[0] | (uint32_t) h[2] << 16, h[1] | (uint32_t) h[3] << 16);
+    fr[48] = make_uint2(h[4] | (uint32_t) h[6] << 16, h[5] | (uint32_t) h[7] << 16);
+    if (c == 0) da[tb] = q.d[tb];
 }
 
 // RoPE mode 0 (ggml.c:7156-7227) + KV append (llama.cpp:996-1008) of the
@@ -461,13 +472,15 @@ bool mm_mfma_supported(const QMatrix & w) {
     return w.qtype == Q4_0 && w.M % TM == 0 && w.K % 256 == 0;
 }
 
-hipError_t launch_mm_mfma(const QMatrix & w, const uint16_t * xh, const float * da, int N, float * y, int ldy,
+size_t mm_act_bytes(int N, int K) { return (size_t) ((N + TN - 1) / TN) * (K / 32) * 4 * 64 * 8; }
+
+hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, int N, float * y, int ldy,
                           int out_tok0, int epi, const uint16_t * silu_tab, hipStream_t s) {
     if (!mm_mfma_supported(w) || N <= 0) return hipErrorInvalidValue;
     MmParams P{};
     P.nib = w.nib; P.scl = (const float4 *) w.scl;
     P.M = w.M; P.K = w.K; P.nb = w.K / 32; P.NC = (P.nb + 31) / 32;
-    P.xh = xh; P.da = da; P.N = N; P.ntt = (N + TN - 1) / TN;
+    P.xm = (const uint2 *) xm; P.da = da; P.N = N; P.ntt = (N + TN - 1) / TN;
     P.y = y; P.ldy = ldy; P.out_tok0 = out_tok0; P.silu_tab = silu_tab;
     const dim3 grid((w.M / TM) * P.ntt);
     switch (epi) {
@@ -479,16 +492,16 @@ hipError_t launch_mm_mfma(const QMatrix & w, const uint16_t * xh, const float * 
     return hipGetLastError();
 }
 
-hipError_t launch_act_f16(const float * x, const float * g, int N, int K, uint16_t * xh, float * da, hipStream_t s) {
+hipError_t launch_act_f16(const float * x, const float * g, int N, int K, void * xm, float * da, hipStream_t s) {
     if (K % 256 || N <= 0) return hipErrorInvalidValue;
-    if (g) LVK_LAUNCH(k_act_q40_f16<true>, dim3(N), dim3(256), 0, s, x, g, K, xh, da);
-    else LVK_LAUNCH(k_act_q40_f16<false>, dim3(N), dim3(256), 0, s, x, g, K, xh, da);
+    if (g) LVK_LAUNCH(k_act_q40_f16<true>, dim3(N), dim3(256), 0, s, x, g, K, (uint2 *) xm, da);
+    else LVK_LAUNCH(k_act_q40_f16<false>, dim3(N), dim3(256), 0, s, x, g, K, (uint2 *) xm, da);
     return hipGetLastError();
 }
 
-hipError_t launch_actq_to_f16(const ActQ & q, int N, int K, uint16_t * xh, float * da, hipStream_t s) {
+hipError_t launch_actq_to_f16(const ActQ & q, int N, int K, void * xm, float * da, hipStream_t s) {
     const long n = (long) N * (K / 32) * 4;
-    LVK_LAUNCH(k_actq_to_f16, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, q, N, K, xh, da);
+    LVK_LAUNCH(k_actq_to_f16, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, q, N, K, (uint2 *) xm, da);
     return hipGetLastError();
 }
 

@@ -78,7 +78,8 @@ void Context::init(const llama_context_params & p) {
     u_ffn = (float *) model.alloc(F * 4);
     {
         const size_t Cp = (C + 63) / 64 * 64, KX = std::max(E, F);
-        xh = (uint16_t *) model.alloc(Cp * KX * 2);
+        xh = (uint16_t *) model.alloc(mm_act_bytes((int) Cp, (int) KX));
+        LVK_HIP(hipMemset(xh, 0, mm_act_bytes((int) Cp, (int) KX)));   // masked slots stay zero
         xda = (float *) model.alloc(Cp * (KX / 32) * 4);
         qkv32 = (float *) model.alloc(C * 3 * E * 4);
         uf = (float *) model.alloc(C * F * 4);

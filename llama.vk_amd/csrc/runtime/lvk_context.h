@@ -50,7 +50,7 @@ struct Context {
     // prompt (N > 1) path: MFMA matmuls with exact block dots (default) or the
     // bit-faithful VALU kernels (prompt_exact; env LVK_PROMPT_EXACT=1)
     bool prompt_exact = false;
-    uint16_t * xh = nullptr;     // [Cpad][max(E,F)] f16 quantized activations (MFMA operand)
+    uint16_t * xh = nullptr;     // masked MFMA B-fragment image of the quantized activations (mm_act_bytes)
     float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales
     float * qkv32 = nullptr;     // [C][3E] Q|K|V rows before RoPE
     float * uf = nullptr;        // [C][F] silu(w1 x) * (w3 x)

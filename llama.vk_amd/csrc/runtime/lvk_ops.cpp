@@ -148,7 +148,8 @@ int lvk_mul_mat_q_mfma(int type, const void * w, int m, int k, const float * g, 
         LVK_HIP(lvk::launch_repack(wd, type, m, k, (uint4 *) q.nib, (void *) q.scl, nullptr));
         float * xd = dv.up(x, (size_t) n * k);
         const float * gd = g ? dv.up(g, (size_t) k) : nullptr;
-        uint16_t * xh = (uint16_t *) dv.get((size_t) n * k * 2);
+        void * xh = dv.get(lvk::mm_act_bytes(n, k));
+        LVK_HIP(hipMemset(xh, 0, lvk::mm_act_bytes(n, k)));
         float * da = (float *) dv.get((size_t) n * nb * 4);
         float * yd = (float *) dv.get((size_t) n * m * 4);
         LVK_HIP(lvk::launch_act_f16(xd, gd, n, k, xh, da, nullptr));
