@@ -61,6 +61,12 @@ LVK_API int lvk_attention(const uint16_t * kc, const uint16_t * vc, const float 
 LVK_API int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
                                  int n_ctx, int n_past, int n, float * out, float * scores_out);
 
+/* lvk_attention through the prompt-batch kernels (attention_prompt.hip: scores +
+ * softmax per 32 query tokens, P.V per 32-dim slice); same result bits.  Needs
+ * head_dim 128, n_ctx % 32 == 0, n_ctx <= 1024. */
+LVK_API int lvk_attention_prompt(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
+                                 int n_ctx, int n_past, int n, float * out);
+
 /* Self-check of the softmax exp: the number of arguments h <= 0 (fp16 bits)
  * where the device's computed fp16(expf(h)) differs from this host's
  * table_exp_f16[h] (ggml.c:2915-2927).  Contexts use the computed exp only when

@@ -1,0 +1,279 @@
+// attention_prompt.hip -- causal self-attention of a prompt batch (N > 1
+// tokens) over the f16 KV cache, bit-faithful to the reference graph
+// (llama.cpp:1010-1061) exactly like attention.hip, but organised for many
+// query tokens: the decode kernel's one-workgroup-per-(token, head) layout
+// re-streams K and V for every token (22 ms of a 512-token 7B prompt).
+//
+//   k_attn_p_scores  grid (H, ceil(N/T)): Q of T tokens in LDS; K streamed
+//                    once in 64-position tiles (a lane quad per position, its
+//                    K row in registers, Q broadcast from LDS); scores
+//                    KQ*scale (ggml_vec_dot_f16 order, ggml.c:1781-1815) in
+//                    LDS; -inf past n_past+t; softmax with the fp16 exp table
+//                    and the exact double sum (ggml.c:7099-7121); P rounded
+//                    to f16 -> global scratch P[h][t][n_ctx].
+//   k_attn_p_pv      grid (H, ceil(N/32), HD/32): V rows of one 32-dim slice
+//                    and P of 32 tokens in LDS; each lane quad owns 4 dims x 4
+//                    tokens (16 dots, 8 AVX accumulators each); leftovers past
+//                    n_kv & ~31 in double (ggml.c:1806-1808); the slice is one
+//                    Q4_0 block of the merged heads: quantize_row_q4_0
+//                    (ggml.c:621-685) fused, written as the Wo input (ActQ and,
+//                    for the MFMA Wo, the masked fragment image).
+#include "lvk_device.h"
+#include "lvk_kernels.h"
+#include "matvec_common.h"
+
+namespace lvk {
+
+namespace {
+
+constexpr int HD = 128;
+
+__device__ __forceinline__ void unpack8(const uint4 v, float f[8]) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        f[2 * k] = f16_to_f32((uint16_t) (w[k] & 0xFFFFu));
+        f[2 * k + 1] = f16_to_f32((uint16_t) (w[k] >> 16));
+    }
+}
+
+// the quad's 4 x 8 accumulators in the AVX2 F32Cx8_REDUCE order (as attention.hip)
+__device__ __forceinline__ float quad_reduce(const float s[8]) {
+    float S[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        const float v0 = quad_bcast<0>(s[l]), v1 = quad_bcast<1>(s[l]);
+        const float v2 = quad_bcast<2>(s[l]), v3 = quad_bcast<3>(s[l]);
+        const float a = v0 + v1, b = v2 + v3;
+        S[l] = a + b;
+    }
+    const float t0 = S[0] + S[4], t1 = S[1] + S[5], t2 = S[2] + S[6], t3 = S[3] + S[7];
+    return (t0 + t1) + (t2 + t3);
+}
+
+// table_exp_f16 (see attention.hip exp_h)
+__device__ __forceinline__ uint16_t exp_h(uint16_t hx, const uint16_t * __restrict__ tab, bool computed) {
+    if (computed && ((hx & 0x8000u) || hx == 0) && (hx & 0x7fffu) <= 0x7c00u)
+        return f32_to_f16((float) exp((double) f16_to_f32(hx)));
+    return tab[hx];
+}
+
+// ---------------------------------------------------------------------------
+// scores + softmax.  T query tokens per workgroup, 256 threads = 64 quads.
+// ---------------------------------------------------------------------------
+template <int T>
+__global__ __launch_bounds__(256) void k_attn_p_scores(const uint16_t * __restrict__ q16, const uint16_t * __restrict__ kc,
+                                                       const uint16_t * __restrict__ exp_tab, const StepParams * sp,
+                                                       int E, int n_ctx, float scale, uint16_t * __restrict__ P,
+                                                       int exp_computed) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int n_past = sp->n_past, N = sp->n_tokens;
+    const int n_kv = n_past + N;
+    const int h = blockIdx.x, t0 = blockIdx.y * T;
+    const int nt = min(T, N - t0);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = tid & 3, quad = tid >> 2;
+    uint4 * qs = (uint4 *) smem;                             // [T][16] uint4: Q rows (f16)
+    float * sc = (float *) (smem + T * 256);                  // [T][n_ctx] scores, then exp values
+    const int lim_hi = n_past + t0 + nt - 1;                 // last unmasked position of the block
+
+    for (int i = tid; i < T * 16; i += 256) {
+        const int t = i >> 4;
+        qs[i] = t < nt ? *((const uint4 *) (q16 + (size_t) (t0 + t) * E + h * HD) + (i & 15)) : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+
+    // ---- scores: quad `quad` owns position p = pb + quad of each 64-position tile ----
+    for (int pb = 0; pb <= lim_hi; pb += 64) {
+        const int p = pb + quad;
+        const bool live = p <= lim_hi;
+        uint4 kr[4];
+        const uint4 * kp = (const uint4 *) (kc + (size_t) min(p, lim_hi) * E + h * HD) + r;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) kr[st] = kp[st * 4];
+        float kf[4][8];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) unpack8(kr[st], kf[st]);
+        for (int t = 0; t < nt; ++t) {
+            float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                float qf[8];
+                unpack8(qs[t * 16 + st * 4 + r], qf);      // broadcast across quads
+#pragma unroll
+                for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(kf[st][l], qf[l], s[l]);
+            }
+            const float kq = quad_reduce(s);
+            if (r == 0 && live) sc[(size_t) t * n_ctx + p] = p <= n_past + t0 + t ? kq * scale : -INFINITY;
+        }
+    }
+    __syncthreads();
+
+    // ---- softmax per token row (ggml.c:7099-7121); wave w owns rows w, w+4, ... ----
+    for (int t = wave; t < nt; t += 4) {
+        float * row = sc + (size_t) t * n_ctx;
+        const int lim = n_past + t0 + t;
+        // positions lim+1 .. n_kv-1 are -inf (ggml.c:7028-7031): max over the live ones
+        float mx = -INFINITY;
+        for (int p = lane; p <= lim; p += 64) { const float v = row[p]; mx = v > mx ? v : mx; }
+        mx = wave_max_f(mx);
+        double sum = 0.0;      // exact in any order: every term is an fp16 value in [0,1]
+        for (int p = lane; p <= lim; p += 64) {
+            const float e = f16_to_f32(exp_h(f32_to_f16(row[p] - mx), exp_tab, exp_computed != 0));
+            sum += (double) e;
+            row[p] = e;
+        }
+        sum = wave_sum_d(sum);
+        const float scl = (float) (1.0 / sum);
+        uint16_t * prow = P + ((size_t) h * N + t0 + t) * n_ctx;
+        const int n_pad = (n_kv + 31) & ~31;
+        for (int p = lane; p < n_pad; p += 64) prow[p] = p <= lim ? f32_to_f16(row[p] * scl) : (uint16_t) 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// P.V for one 32-dim slice (one Q4_0 block of the merged heads) and 32 tokens.
+// Quad (qd, qt): dims 4qd..4qd+3, tokens 4qt..4qt+3 of the slice / block.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_attn_p_pv(const uint16_t * __restrict__ vc, const uint16_t * __restrict__ P,
+                                                   const StepParams * sp, int E, int n_ctx, ActQ out, uint2 * xm,
+                                                   float * xda, float * __restrict__ out_f32) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int n_past = sp->n_past, N = sp->n_tokens;
+    const int n_kv = n_past + N;
+    const int h = blockIdx.x, t0 = blockIdx.y * 32, ds = blockIdx.z;
+    const int nt = min(32, N - t0);
+    const int tid = threadIdx.x, r = tid & 3, quad = tid >> 2;
+    const int qd = quad & 7, qt = quad >> 3;
+    const int n_pad = (n_kv + 31) & ~31;
+    const int np = n_kv & ~31;
+    const int lim_hi = n_past + t0 + nt - 1;
+    const int nsteps = min(np, lim_hi + 1 + 31) / 32;        // steps holding at least one unmasked position
+    const int nfill = min(n_pad, (lim_hi + 32) & ~31);        // positions any dot of the block reads
+    uint16_t * vl = (uint16_t *) smem;                         // [32 dims][n_pad]
+    uint16_t * pl = vl + (size_t) 32 * n_pad;                  // [32 tokens][n_pad]
+    const int d0 = h * HD + ds * 32;
+
+    // stage V rows d0..d0+31 and the P rows of the block (16-byte pieces)
+    const int per = nfill / 8;
+    for (int i = tid; i < 32 * per; i += 256) {
+        const int row = i / per, c = i % per;
+        ((uint4 *) (vl + (size_t) row * n_pad))[c] = ((const uint4 *) (vc + (size_t) (d0 + row) * n_ctx))[c];
+        ((uint4 *) (pl + (size_t) row * n_pad))[c] =
+            row < nt ? ((const uint4 *) (P + ((size_t) h * N + t0 + row) * n_ctx))[c] : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+
+    float s[4][4][8];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) s[a][b][l] = 0.0f;
+    for (int st = 0; st < nsteps; ++st) {
+        float vf[4][8], pf[4][8];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) unpack8(*((const uint4 *) (vl + (size_t) (4 * qd + a) * n_pad + st * 32) + r), vf[a]);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) unpack8(*((const uint4 *) (pl + (size_t) (4 * qt + b) * n_pad + st * 32) + r), pf[b]);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int l = 0; l < 8; ++l) s[a][b][l] = __builtin_fmaf(vf[a][l], pf[b][l], s[a][b][l]);
+    }
+    // reduce + double leftovers (ggml.c:1806-1808), in position order
+    float o[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const float res = quad_reduce(s[a][b]);
+            const int t = 4 * qt + b;
+            const int lim = n_past + t0 + t;
+            float v = res;
+            if (np < n_kv && np <= lim) {
+                double sumf = (double) res;
+                const uint16_t * vr = vl + (size_t) (4 * qd + a) * n_pad;
+                const uint16_t * pr = pl + (size_t) t * n_pad;
+                for (int p = np; p < n_kv; ++p) {
+                    const float prod = f16_to_f32(vr[p]) * f16_to_f32(pr[p]);
+                    sumf += (double) prod;
+                }
+                v = (float) sumf;
+            }
+            o[a][b] = v;
+        }
+    // ---- merged heads: this slice is one Q4_0 block per token; quantize (ggml.c:621-685) ----
+    __syncthreads();
+    float * ob = (float *) smem;                               // [32 tokens][33]
+    if (r == 0) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) ob[(4 * qt + b) * 33 + 4 * qd + a] = o[a][b];
+    }
+    __syncthreads();
+    // one 32-lane half-wave per token: 8 tokens per pass
+    const int e = tid & 31;
+    const int nb = E / 32, blk = d0 / 32;
+    for (int t = tid >> 5; t < nt; t += 8) {
+        const float v = ob[t * 33 + e];
+        const int tok = t0 + t;
+        if (out_f32) out_f32[(size_t) tok * E + d0 + e] = v;
+        float amax = fabsf(v);
+        for (int o2 = 16; o2 > 0; o2 >>= 1) { const float w = __shfl_xor(amax, o2); amax = w > amax ? w : amax; }
+        const float dd = amax / 7.0f;
+        const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;
+        const uint32_t qq = (uint32_t) ((int) __builtin_rintf(v * id) + 8) & 15u;
+        uint32_t part = qq << (4 * (e & 7));
+        part |= __shfl_xor(part, 1);
+        part |= __shfl_xor(part, 2);
+        part |= __shfl_xor(part, 4);
+        // the reference block (d + 16 nibble bytes): lanes e = 0, 8, 16, 24 hold its 4 words
+        const uint32_t w0 = __shfl(part, (tid & 32) + 0), w1 = __shfl(part, (tid & 32) + 8);
+        const uint32_t w2 = __shfl(part, (tid & 32) + 16), w3 = __shfl(part, (tid & 32) + 24);
+        if (e == 0) {
+            out.d[(size_t) tok * out.nb + blk] = dd;
+            out.qs[(size_t) tok * out.nb + blk] = make_uint4(w0, w1, w2, w3);
+        }
+        if (xm && e < 4) {
+            // the masked MFMA fragment image of the Wo input (mm_mfma.hip): group c = e holds
+            // elements 8c..8c+7 = word c; chain 2c -> lane n, chain 2c+1 -> lane 48 + n
+            const uint32_t word = e == 0 ? w0 : e == 1 ? w1 : e == 2 ? w2 : w3;
+            uint16_t hh[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                hh[k] = __builtin_bit_cast(uint16_t, (_Float16) (float) ((int) ((word >> (4 * k)) & 15u) - 8));
+            uint2 * fr = xm + ((size_t) ((tok >> 4) * nb + blk) * 4 + e) * 64 + (tok & 15);
+            fr[0] = make_uint2(hh[0] | (uint32_t) hh[2] << 16, hh[1] | (uint32_t) hh[3] << 16);
+            fr[48] = make_uint2(hh[4] | (uint32_t) hh[6] << 16, hh[5] | (uint32_t) hh[7] << 16);
+            if (e == 0) xda[(size_t) tok * nb + blk] = dd;
+        }
+    }
+}
+
+}  // namespace
+
+bool attention_prompt_supported(int n_embd, int n_head, int n_ctx) {
+    return n_embd / n_head == HD && n_ctx % 32 == 0 && n_ctx <= 1024;
+}
+
+hipError_t launch_attention_prompt(const AttnLaunch & A, uint16_t * p_scratch, void * xm, float * xda,
+                                   hipStream_t s) {
+    if (!attention_prompt_supported(A.n_embd, A.n_head, A.n_ctx) || A.out_qtype != Q4_0) return hipErrorNotSupported;
+    const float scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
+    constexpr int T = 32;
+    const size_t lds1 = (size_t) T * 256 + (size_t) T * A.n_ctx * 4;
+    LVK_LAUNCH(k_attn_p_scores<T>, dim3(A.n_head, (A.n_tokens + T - 1) / T), dim3(256), lds1, s, A.q16, A.kc,
+               A.exp_tab, A.sp, A.n_embd, A.n_ctx, scale, p_scratch, A.exp_computed);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t lds2 = (size_t) 64 * A.n_ctx * 2;
+    LVK_LAUNCH(k_attn_p_pv, dim3(A.n_head, (A.n_tokens + 31) / 32, HD / 32), dim3(256), lds2, s, A.vc, p_scratch,
+               A.sp, A.n_embd, A.n_ctx, A.out, (uint2 *) xm, xda, A.out_f32);
+    return hipGetLastError();
+}
+
+}  // namespace lvk

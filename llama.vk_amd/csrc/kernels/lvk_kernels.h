@@ -126,6 +126,13 @@ struct AttnLaunch {
     int exp_computed = 0;     // 1: softmax computes exp in registers (only after exp_check found 0 mismatches)
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
+// prompt batches (N > 1, Q4_0 output): scores+softmax per (head, 32 tokens) then
+// P.V per (head, 32 tokens, 32 dims) with the Wo quantization fused
+// (attention_prompt.hip).  p_scratch: H*N*n_ctx f16; xm/xda (optional): also
+// write the Wo input as the MFMA fragment image (mm_mfma.hip).
+bool attention_prompt_supported(int n_embd, int n_head, int n_ctx);
+hipError_t launch_attention_prompt(const AttnLaunch & A, uint16_t * p_scratch, void * xm, float * xda,
+                                   hipStream_t s);
 // count (into *bad_d) the softmax arguments h <= 0 whose computed exp differs
 // from exp_tab[h]; 0 means the computed path reproduces the host table exactly
 hipError_t exp_check(const uint16_t * exp_tab, int * bad_d, hipStream_t s);

@@ -202,8 +202,15 @@ void Context::enqueue_forward(int n, bool last_only) {
             });
             AttnLaunch at{q16, kcl, vcl, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
             at.exp_computed = exp_computed;
-            timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
-            timed_launch(K_WO, 0, [&] { return launch_actq_to_f16(aq_attn, n, E, xh, xda, stream); });
+            if (attention_prompt_supported(E, H, n_ctx)) {
+                // writes the Wo input in both forms (ActQ and the MFMA fragment image)
+                timed_launch(K_ATTN, 0, [&] {
+                    return launch_attention_prompt(at, (uint16_t *) scores, xh, xda, stream);
+                });
+            } else {
+                timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
+                timed_launch(K_WO, 0, [&] { return launch_actq_to_f16(aq_attn, n, E, xh, xda, stream); });
+            }
             timed_launch(K_WO, qbytes(ly.wo), [&] {
                 return launch_mm_mfma(ly.wo, xh, xda, n, x, E, 0, EPI_RESID, nullptr, stream);
             });
@@ -247,7 +254,10 @@ void Context::enqueue_forward(int n, bool last_only) {
         timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
         AttnLaunch at{q16, kc + il * CE, vc + il * CE, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
         at.exp_computed = exp_computed;
-        timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
+        if (n > 1 && model.qtype == Q4_0 && attention_prompt_supported(E, H, n_ctx))
+            timed_launch(K_ATTN, 0, [&] { return launch_attention_prompt(at, (uint16_t *) scores, nullptr, nullptr, stream); });
+        else
+            timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
         MvLaunch b;
         b.w = ly.wo; b.xq = aq_attn; b.y = x; b.sp = sp_d; b.n_tokens = n;
         timed_launch(K_WO, qbytes(ly.wo), [&] { return mv_launch(b, PRO_ACTQ, EPI_RESID, stream); });

@@ -166,8 +166,24 @@ int lvk_attention(const uint16_t * kc, const uint16_t * vc, const float * q, int
     return lvk_attention_scores(kc, vc, q, n_embd, n_head, n_ctx, n_past, n, out, nullptr);
 }
 
+static int attention_impl(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
+                          int n_ctx, int n_past, int n, float * out, float * scores_out, bool prompt);
+
 int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
                          int n_ctx, int n_past, int n, float * out, float * scores_out) {
+    return attention_impl(kc, vc, q, n_embd, n_head, n_ctx, n_past, n, out, scores_out, false);
+}
+
+int lvk_attention_prompt(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
+                         int n_ctx, int n_past, int n, float * out) {
+    if (!lvk::attention_prompt_supported(n_embd, n_head, n_ctx))
+        return fail(__func__, "needs head_dim 128, n_ctx % 32 == 0, n_ctx <= 1024");
+    return attention_impl(kc, vc, q, n_embd, n_head, n_ctx, n_past, n, out, nullptr, true);
+}
+
+static int attention_impl(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
+                          int n_ctx, int n_past, int n, float * out, float * scores_out, bool prompt) {
+    const char * fn = prompt ? "lvk_attention_prompt" : "lvk_attention";
     try {
         Dev dv;
         const size_t CE = (size_t) n_ctx * n_embd;
@@ -201,7 +217,8 @@ int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float *
         uint16_t * pd = nullptr;
         if (scores_out) pd = (uint16_t *) dv.get((size_t) n * n_head * n_ctx * 2);
         A.p16_out = pd;
-        LVK_HIP(lvk::launch_attention(A, nullptr));
+        if (prompt) LVK_HIP(lvk::launch_attention_prompt(A, (uint16_t *) A.scores, nullptr, nullptr, nullptr));
+        else LVK_HIP(lvk::launch_attention(A, nullptr));
         LVK_HIP(hipMemcpy(out, od, (size_t) n * n_embd * 4, hipMemcpyDeviceToHost));
         if (scores_out) {
             LVK_HIP(hipMemcpy(scores_out, A.scores, (size_t) n * n_head * n_ctx * 4, hipMemcpyDeviceToHost));
@@ -210,7 +227,7 @@ int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float *
                               hipMemcpyDeviceToHost));
         }
         return 0;
-    } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+    } catch (const lvk::Error & e) { return fail(fn, e.msg); }
 }
 
 int lvk_exp_table_mismatches(void) {

@@ -119,6 +119,25 @@ def test_attention(lvk, oracle, monkeypatch, exp_path, n_past, N, C, qs):
     assert np.array_equal(bits(got), bits(want))
 
 
+@pytest.mark.parametrize("exp_path", ["computed", "table"])
+@pytest.mark.parametrize("n_past,N,C,qs", [(0, 2, 256, 1), (40, 3, 256, 1), (60, 37, 256, 1), (0, 64, 256, 1),
+                                           (10, 100, 256, 8), (0, 512, 512, 1), (100, 300, 512, 4),
+                                           (511, 2, 1024, 4), (1000, 3, 1024, 1), (64, 900, 1024, 1)])
+def test_attention_prompt_kernels(lvk, oracle, monkeypatch, exp_path, n_past, N, C, qs):
+    """the prompt-batch attention (attention_prompt.hip) is bit-identical to the reference graph"""
+    if exp_path == "table":
+        monkeypatch.setenv("LVK_EXP_TABLE", "1")
+    E, H = 512, 4
+    rng = np.random.default_rng(n_past * 17 + N + C)
+    kc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
+    vc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
+    q = (qs * rng.standard_normal(N * E)).astype(np.float32)
+    got = lvk.attention_prompt(kc, vc, q, E, H, C, n_past, N)
+    want = np.zeros(N * E, np.float32)
+    oracle.lib.orc_attention(kc, vc, q, E, H, C, n_past, N, want)
+    assert np.array_equal(bits(got), bits(want))
+
+
 def test_rms_norm_mul(lvk, oracle):
     rng = np.random.default_rng(3)
     x = (rng.standard_normal((4, 4096)) * 3).astype(np.float32)
