@@ -67,10 +67,17 @@ LVK_API int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const
 LVK_API int lvk_attention_prompt(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
                                  int n_ctx, int n_past, int n, float * out);
 
+/* lvk_attention for one token (n = 1) through the decode kernels
+ * (attention_decode.hip: scores per 64 positions, softmax + P.V per 32-dim
+ * slice); same result bits.  Needs head_dim 128, n_ctx % 64 == 0, n_ctx <= 2048. */
+LVK_API int lvk_attention_decode(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
+                                 int n_ctx, int n_past, float * out);
+
 /* Self-check of the softmax exp: the number of arguments h <= 0 (fp16 bits)
- * where the device's computed fp16(expf(h)) differs from this host's
- * table_exp_f16[h] (ggml.c:2915-2927).  Contexts use the computed exp only when
- * this is 0 (env LVK_EXP_TABLE forces the table).  -1 on error. */
+ * where the device's computed fp16(exp(h)) differs from this host's
+ * table_exp_f16[h] (ggml.c:2915-2927) -- 0 when the device expf reproduces it,
+ * else the count of the double-precision exp.  Contexts compute exp only in a
+ * mode with 0 mismatches (env LVK_EXP_TABLE forces the table).  -1 on error. */
 LVK_API int lvk_exp_table_mismatches(void);
 
 /* y[t] = g * rms_norm(x[t]) (ggml.c:6024-6080 + llama.cpp:984) */

@@ -69,16 +69,14 @@ __device__ __forceinline__ float quad_f16dot_reduce(const float s[8]) {
 // arguments softmax produces (h <= 0, not NaN), computed in double and rounded
 // to f32 then f16 -- the two roundings the table went through.  Used only when
 // exp_check() has shown it equal to the uploaded host table on every such h.
-__device__ __forceinline__ uint16_t exp_h(uint16_t hx, const uint16_t * __restrict__ tab, bool computed) {
-    if (computed && ((hx & 0x8000u) || hx == 0) && (hx & 0x7fffu) <= 0x7c00u)
-        return f32_to_f16((float) exp((double) f16_to_f32(hx)));
-    return tab[hx];
-}
 
+// bad[m-1]: arguments where mode m (1 double, 2 device expf) differs from the table
 __global__ void k_exp_check(const uint16_t * __restrict__ tab, int * __restrict__ bad) {
     const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
-    if (h < 65536u && ((h & 0x8000u) || h == 0) && (h & 0x7fffu) <= 0x7c00u)
-        if (exp_h((uint16_t) h, tab, true) != tab[h]) atomicAdd(bad, 1);
+    if (h < 65536u && ((h & 0x8000u) || h == 0) && (h & 0x7fffu) <= 0x7c00u) {
+        if (exp_f16((uint16_t) h, tab, 1) != tab[h]) atomicAdd(bad, 1);
+        if (exp_f16((uint16_t) h, tab, 2) != tab[h]) atomicAdd(bad + 1, 1);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -191,7 +189,7 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
         const float v = sc[p];
         float e = 0.0f;
         if (v != -INFINITY) {
-            e = f16_to_f32(exp_h(f32_to_f16(v - mx), exp_tab, exp_computed != 0));
+            e = f16_to_f32(exp_f16(f32_to_f16(v - mx), exp_tab, exp_computed));
             sum += (double) e;
         }
         sc[p] = e;
@@ -306,7 +304,7 @@ void * lvk_probe_atrace() { void * p = nullptr; (void) hipGetSymbolAddress(&p, H
 #endif
 
 hipError_t exp_check(const uint16_t * exp_tab, int * bad_d, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(bad_d, 0, sizeof(int), s);
+    hipError_t e = hipMemsetAsync(bad_d, 0, 2 * sizeof(int), s);
     if (e != hipSuccess) return e;
     k_exp_check<<<256, 256, 0, s>>>(exp_tab, bad_d);
     return hipGetLastError();

@@ -51,12 +51,6 @@ __device__ __forceinline__ float quad_reduce(const float s[8]) {
     return (t0 + t1) + (t2 + t3);
 }
 
-// table_exp_f16 (see attention.hip exp_h)
-__device__ __forceinline__ uint16_t exp_h(uint16_t hx, const uint16_t * __restrict__ tab, bool computed) {
-    if (computed && ((hx & 0x8000u) || hx == 0) && (hx & 0x7fffu) <= 0x7c00u)
-        return f32_to_f16((float) exp((double) f16_to_f32(hx)));
-    return tab[hx];
-}
 
 // ---------------------------------------------------------------------------
 // scores + softmax.  T query tokens per workgroup, 256 threads = 64 quads.
@@ -118,7 +112,7 @@ __global__ __launch_bounds__(256) void k_attn_p_scores(const uint16_t * __restri
         mx = wave_max_f(mx);
         double sum = 0.0;      // exact in any order: every term is an fp16 value in [0,1]
         for (int p = lane; p <= lim; p += 64) {
-            const float e = f16_to_f32(exp_h(f32_to_f16(row[p] - mx), exp_tab, exp_computed != 0));
+            const float e = f16_to_f32(exp_f16(f32_to_f16(row[p] - mx), exp_tab, exp_computed));
             sum += (double) e;
             row[p] = e;
         }
@@ -265,12 +259,15 @@ hipError_t launch_attention_prompt(const AttnLaunch & A, uint16_t * p_scratch, v
     if (!attention_prompt_supported(A.n_embd, A.n_head, A.n_ctx) || A.out_qtype != Q4_0) return hipErrorNotSupported;
     const float scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
     constexpr int T = 32;
+    EventSplit ev;
+    ev.first();
     const size_t lds1 = (size_t) T * 256 + (size_t) T * A.n_ctx * 4;
     LVK_LAUNCH(k_attn_p_scores<T>, dim3(A.n_head, (A.n_tokens + T - 1) / T), dim3(256), lds1, s, A.q16, A.kc,
                A.exp_tab, A.sp, A.n_embd, A.n_ctx, scale, p_scratch, A.exp_computed);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds2 = (size_t) 64 * A.n_ctx * 2;
+    ev.last();
     LVK_LAUNCH(k_attn_p_pv, dim3(A.n_head, (A.n_tokens + 31) / 32, HD / 32), dim3(256), lds2, s, A.vc, p_scratch,
                A.sp, A.n_embd, A.n_ctx, A.out, (uint2 *) xm, xda, A.out_f32);
     return hipGetLastError();

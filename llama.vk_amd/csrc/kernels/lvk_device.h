@@ -27,6 +27,20 @@ __device__ __forceinline__ float f16_to_f32(uint16_t h) {
     return (float) __builtin_bit_cast(_Float16, h);   // exact
 }
 
+// table_exp_f16[h] (ggml.c:2915-2927: fp16(expf(fp16->f32(h))), built with the
+// host's glibc) for the arguments softmax produces (h <= 0, not NaN).
+// mode 0 reads the uploaded table; mode 1 computes exp in double, mode 2 with
+// the device expf, both rounded to f32 then f16 like the table.  A context
+// uses mode 2 or 1 only after exp_check() found it equal to the table on every
+// such h (lvk_exp_table_mismatches).
+__device__ __forceinline__ uint16_t exp_f16(uint16_t hx, const uint16_t * __restrict__ tab, int mode) {
+    if (mode != 0 && ((hx & 0x8000u) || hx == 0) && (hx & 0x7fffu) <= 0x7c00u) {
+        const float x = f16_to_f32(hx);
+        return f32_to_f16(mode == 2 ? expf(x) : (float) exp((double) x));
+    }
+    return tab[hx];
+}
+
 // quad_perm DPP broadcast of lane k (0..3) of each 4-lane quad
 template <int K>
 __device__ __forceinline__ float quad_bcast(float v) {

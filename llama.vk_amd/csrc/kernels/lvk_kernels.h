@@ -18,10 +18,18 @@ struct LaunchEvents {
     hipEvent_t stop = nullptr;
 };
 extern thread_local LaunchEvents g_launch_events;
+// a launcher of several kernels times them as one: the start event goes to the
+// first kernel, the stop event to the last
+struct EventSplit {
+    LaunchEvents saved = g_launch_events;
+    void first() { g_launch_events = {saved.start, nullptr}; }
+    void last() { g_launch_events = {nullptr, saved.stop}; }
+    ~EventSplit() { g_launch_events = saved; }
+};
 
 #define LVK_LAUNCH(kern, grid, block, lds, stream, ...)                                                        \
     do {                                                                                                       \
-        if (::lvk::g_launch_events.start)                                                                      \
+        if (::lvk::g_launch_events.start || ::lvk::g_launch_events.stop)                                       \
             hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ::lvk::g_launch_events.start,                \
                                   ::lvk::g_launch_events.stop, 0, __VA_ARGS__);                                \
         else                                                                                                   \
@@ -123,7 +131,7 @@ struct AttnLaunch {
     int n_tokens, n_embd, n_head, n_ctx;
     float * out_f32 = nullptr; // optional: also store the unquantized merged heads [N][E]
     uint16_t * p16_out = nullptr; // optional (debug): f16 probabilities [N][H][n_ctx]
-    int exp_computed = 0;     // 1: softmax computes exp in registers (only after exp_check found 0 mismatches)
+    int exp_computed = 0;     // exp mode (lvk_device.h exp_f16): 0 table, 1 double, 2 f32 -- nonzero only after exp_check
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
 // prompt batches (N > 1, Q4_0 output): scores+softmax per (head, 32 tokens) then
@@ -133,9 +141,17 @@ hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
 bool attention_prompt_supported(int n_embd, int n_head, int n_ctx);
 hipError_t launch_attention_prompt(const AttnLaunch & A, uint16_t * p_scratch, void * xm, float * xda,
                                    hipStream_t s);
-// count (into *bad_d) the softmax arguments h <= 0 whose computed exp differs
-// from exp_tab[h]; 0 means the computed path reproduces the host table exactly
+// count into bad_d[0] / bad_d[1] the softmax arguments h <= 0 whose exp computed in
+// double / with the device expf differs from exp_tab[h]; 0 means that mode
+// reproduces the host table exactly
 hipError_t exp_check(const uint16_t * exp_tab, int * bad_d, hipStream_t s);
+// single-token attention, 4 workgroups per head in one launch (attention_decode.hip):
+// the head's scores are exchanged through `gran` (attention_decode_scratch_bytes,
+// ZEROED before the first layer of every token) tagged with `epoch` (layer + 1,
+// never 0).  Needs A.n_tokens == 1.
+bool attention_decode_supported(int n_embd, int n_head, int n_ctx);
+size_t attention_decode_scratch_bytes(int n_head, int n_ctx);
+hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned epoch, hipStream_t s);
 
 // one-time weight repack: file-layout rows (ggml blocks) -> quad-sliced image
 // interleave4: src_rows holds two (M/2)-row matrices A then B; the image

@@ -43,6 +43,22 @@ void host_fp16_tables(std::vector<uint16_t> & te, std::vector<uint16_t> & ts) {
     }
 }
 
+// the softmax may compute exp instead of reading the table, but only in a mode
+// that reproduces this host's table on every argument it can see: 2 (device
+// expf) if exact, else 1 (double exp) if exact, else 0 (table).  LVK_EXP_TABLE
+// forces the table.
+int pick_exp_mode(const uint16_t * exp_tab_d) {
+    if (getenv("LVK_EXP_TABLE")) return 0;
+    int * bad_d = nullptr;
+    LVK_HIP(hipMalloc((void **) &bad_d, 2 * sizeof(int)));
+    int bad[2] = {-1, -1};
+    const hipError_t e1 = exp_check(exp_tab_d, bad_d, nullptr);
+    const hipError_t e2 = e1 == hipSuccess ? hipMemcpy(bad, bad_d, sizeof(bad), hipMemcpyDeviceToHost) : e1;
+    (void) hipFree(bad_d);
+    LVK_HIP(e2);
+    return bad[1] == 0 ? 2 : bad[0] == 0 ? 1 : 0;
+}
+
 Context::~Context() {
     if (graph_exec) (void) hipGraphExecDestroy(graph_exec);
     if (graph) (void) hipGraphDestroy(graph);
@@ -84,6 +100,8 @@ void Context::init(const llama_context_params & p) {
         qkv32 = (float *) model.alloc(C * 3 * E * 4);
         uf = (float *) model.alloc(C * F * 4);
         prompt_exact = getenv("LVK_PROMPT_EXACT") && atoi(getenv("LVK_PROMPT_EXACT")) != 0;
+        old_attention = getenv("LVK_ATTN_V1") && atoi(getenv("LVK_ATTN_V1")) != 0;
+        attn_gran = model.alloc(attention_decode_scratch_bytes((int) H, (int) C));
     }
     logits_d = (float *) model.alloc(C * V * 4);
     emb_d = (float *) model.alloc(E * 4);
@@ -99,16 +117,7 @@ void Context::init(const llama_context_params & p) {
     silu_tab = (uint16_t *) model.alloc(65536 * 2);
     LVK_HIP(hipMemcpy(exp_tab, te.data(), 65536 * 2, hipMemcpyHostToDevice));
     LVK_HIP(hipMemcpy(silu_tab, ts.data(), 65536 * 2, hipMemcpyHostToDevice));
-    {
-        // the softmax may compute exp instead of reading the table, but only if
-        // that reproduces this host's table on every argument it can see
-        int * bad_d = (int *) model.alloc(sizeof(int));
-        int bad = -1;
-        LVK_HIP(exp_check(exp_tab, bad_d, nullptr));
-        LVK_HIP(hipMemcpy(&bad, bad_d, sizeof(int), hipMemcpyDeviceToHost));
-        exp_computed = bad == 0 ? 1 : 0;
-        if (getenv("LVK_EXP_TABLE")) exp_computed = 0;
-    }
+    exp_computed = pick_exp_mode(exp_tab);
     // RoPE cos/sin table (ggml.c:7209-7213): theta = powf(10000, -i0/n_dims), angle = p*theta
     std::vector<float2> rt(C * (hd / 2));
     for (size_t pos = 0; pos < C; ++pos)
@@ -171,7 +180,8 @@ static hipError_t mv_launch(const MvLaunch & L, int pro, int epi, hipStream_t s)
 
 // prompt batches go through the MFMA matmuls when every matrix of the model fits them
 bool Context::use_mfma(int n) const {
-    if (n <= 1 || prompt_exact || model.qtype != Q4_0) return false;
+    // below 16 tokens the per-row VALU kernels win (the MFMA tile is 16 tokens wide)
+    if (n < 16 || prompt_exact || model.qtype != Q4_0) return false;
     for (const Layer & ly : model.layers)
         if (!mm_mfma_supported(ly.wqkv) || !mm_mfma_supported(ly.wo) || !mm_mfma_supported(ly.w13) ||
             !mm_mfma_supported(ly.w2))
@@ -243,6 +253,9 @@ void Context::enqueue_forward(int n, bool last_only) {
     }
     // single-token FFN: W1|W3 hands silu(w1 x)*(w3 x) to W2 in f32, W2 quantizes it
     const bool ffn_f32 = n == 1 && model.qtype == Q4_0 && matvec_cu_supported(E) && matvec_cu_supported(F);
+    if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx))
+        // the decode attention's score granules carry epoch = layer + 1: zero them once per token
+        LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes(H, n_ctx), stream));
     if (model.has_embed)
         timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_d, n, x, stream); });
     for (size_t il = 0; il < model.layers.size(); ++il) {
@@ -256,6 +269,8 @@ void Context::enqueue_forward(int n, bool last_only) {
         at.exp_computed = exp_computed;
         if (n > 1 && model.qtype == Q4_0 && attention_prompt_supported(E, H, n_ctx))
             timed_launch(K_ATTN, 0, [&] { return launch_attention_prompt(at, (uint16_t *) scores, nullptr, nullptr, stream); });
+        else if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx))
+            timed_launch(K_ATTN, 0, [&] { return launch_attention_decode(at, attn_gran, (unsigned) il + 1, stream); });
         else
             timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
         MvLaunch b;

@@ -39,7 +39,7 @@ struct Context {
     float * logits_d = nullptr;  // [n_ctx][V]
     float * emb_d = nullptr;     // [E]
     uint16_t * exp_tab = nullptr;
-    int exp_computed = 0;     // softmax exp computed in registers (verified equal to exp_tab)
+    int exp_computed = 0;     // softmax exp mode (exp_f16: 0 table, 1 double, 2 f32; verified equal to exp_tab)
     uint16_t * silu_tab = nullptr;
     float2 * rope = nullptr;     // [n_ctx][hd/2]
     StepParams * sp_d = nullptr;
@@ -50,6 +50,8 @@ struct Context {
     // prompt (N > 1) path: MFMA matmuls with exact block dots (default) or the
     // bit-faithful VALU kernels (prompt_exact; env LVK_PROMPT_EXACT=1)
     bool prompt_exact = false;
+    bool old_attention = false;
+    void * attn_gran = nullptr;  // [H][n_ctx] {tag, score} granules of the decode attention  // env LVK_ATTN_V1=1: single-token evals on the one-kernel attention.hip
     uint16_t * xh = nullptr;     // masked MFMA B-fragment image of the quantized activations (mm_act_bytes)
     float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales
     float * qkv32 = nullptr;     // [C][3E] Q|K|V rows before RoPE
@@ -95,6 +97,8 @@ struct Context {
 };
 
 int64_t now_us();
+// exp mode of the softmax kernels (lvk_device.h exp_f16): 2, 1 or 0 after a device self-check
+int pick_exp_mode(const uint16_t * exp_tab_d);
 // fp16 exp / silu tables (ggml.c:2915-2927) built with this host's glibc expf
 void host_fp16_tables(std::vector<uint16_t> & exp_tab, std::vector<uint16_t> & silu_tab);
 

@@ -167,23 +167,30 @@ int lvk_attention(const uint16_t * kc, const uint16_t * vc, const float * q, int
 }
 
 static int attention_impl(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
-                          int n_ctx, int n_past, int n, float * out, float * scores_out, bool prompt);
+                          int n_ctx, int n_past, int n, float * out, float * scores_out, int kind);
 
 int lvk_attention_scores(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
                          int n_ctx, int n_past, int n, float * out, float * scores_out) {
-    return attention_impl(kc, vc, q, n_embd, n_head, n_ctx, n_past, n, out, scores_out, false);
+    return attention_impl(kc, vc, q, n_embd, n_head, n_ctx, n_past, n, out, scores_out, 0);
 }
 
 int lvk_attention_prompt(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
                          int n_ctx, int n_past, int n, float * out) {
     if (!lvk::attention_prompt_supported(n_embd, n_head, n_ctx))
         return fail(__func__, "needs head_dim 128, n_ctx % 32 == 0, n_ctx <= 1024");
-    return attention_impl(kc, vc, q, n_embd, n_head, n_ctx, n_past, n, out, nullptr, true);
+    return attention_impl(kc, vc, q, n_embd, n_head, n_ctx, n_past, n, out, nullptr, 1);
+}
+
+int lvk_attention_decode(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
+                         int n_ctx, int n_past, float * out) {
+    if (!lvk::attention_decode_supported(n_embd, n_head, n_ctx))
+        return fail(__func__, "needs head_dim 128, n_ctx % 64 == 0, n_ctx <= 2048");
+    return attention_impl(kc, vc, q, n_embd, n_head, n_ctx, n_past, 1, out, nullptr, 2);
 }
 
 static int attention_impl(const uint16_t * kc, const uint16_t * vc, const float * q, int n_embd, int n_head,
-                          int n_ctx, int n_past, int n, float * out, float * scores_out, bool prompt) {
-    const char * fn = prompt ? "lvk_attention_prompt" : "lvk_attention";
+                          int n_ctx, int n_past, int n, float * out, float * scores_out, int kind) {
+    const char * fn = kind == 1 ? "lvk_attention_prompt" : kind == 2 ? "lvk_attention_decode" : "lvk_attention";
     try {
         Dev dv;
         const size_t CE = (size_t) n_ctx * n_embd;
@@ -203,13 +210,7 @@ static int attention_impl(const uint16_t * kc, const uint16_t * vc, const float 
         std::vector<uint16_t> te, ts;
         lvk::host_fp16_tables(te, ts);
         A.exp_tab = dv.up(te.data(), te.size());
-        {
-            int * bad_d = (int *) dv.get(sizeof(int));
-            int bad = -1;
-            LVK_HIP(lvk::exp_check(A.exp_tab, bad_d, nullptr));
-            LVK_HIP(hipMemcpy(&bad, bad_d, sizeof(int), hipMemcpyDeviceToHost));
-            A.exp_computed = (bad == 0 && !getenv("LVK_EXP_TABLE")) ? 1 : 0;
-        }
+        A.exp_computed = lvk::pick_exp_mode(A.exp_tab);
         A.sp = dv.up(&sp, 1);
         A.n_tokens = n; A.n_embd = n_embd; A.n_head = n_head; A.n_ctx = n_ctx;
         float * od = (float *) dv.get((size_t) n * n_embd * 4);
@@ -217,7 +218,12 @@ static int attention_impl(const uint16_t * kc, const uint16_t * vc, const float 
         uint16_t * pd = nullptr;
         if (scores_out) pd = (uint16_t *) dv.get((size_t) n * n_head * n_ctx * 2);
         A.p16_out = pd;
-        if (prompt) LVK_HIP(lvk::launch_attention_prompt(A, (uint16_t *) A.scores, nullptr, nullptr, nullptr));
+        if (kind == 1) LVK_HIP(lvk::launch_attention_prompt(A, (uint16_t *) A.scores, nullptr, nullptr, nullptr));
+        else if (kind == 2) {
+            void * gran = dv.get(lvk::attention_decode_scratch_bytes(n_head, n_ctx));
+            LVK_HIP(hipMemset(gran, 0, lvk::attention_decode_scratch_bytes(n_head, n_ctx)));
+            LVK_HIP(lvk::launch_attention_decode(A, gran, 1, nullptr));
+        }
         else LVK_HIP(lvk::launch_attention(A, nullptr));
         LVK_HIP(hipMemcpy(out, od, (size_t) n * n_embd * 4, hipMemcpyDeviceToHost));
         if (scores_out) {
@@ -236,11 +242,11 @@ int lvk_exp_table_mismatches(void) {
         std::vector<uint16_t> te, ts;
         lvk::host_fp16_tables(te, ts);
         const uint16_t * tab = dv.up(te.data(), te.size());
-        int * bad_d = (int *) dv.get(sizeof(int));
-        int bad = -1;
+        int * bad_d = (int *) dv.get(2 * sizeof(int));
+        int bad[2] = {-1, -1};
         LVK_HIP(lvk::exp_check(tab, bad_d, nullptr));
-        LVK_HIP(hipMemcpy(&bad, bad_d, sizeof(int), hipMemcpyDeviceToHost));
-        return bad;
+        LVK_HIP(hipMemcpy(bad, bad_d, sizeof(bad), hipMemcpyDeviceToHost));
+        return bad[1] == 0 ? 0 : bad[0];     // the computed exp a context would use (f32, else double)
     } catch (const std::exception & e) {
         return fail("lvk_exp_table_mismatches", e.what());
     }

@@ -87,6 +87,7 @@ _sig("lvk_mul_mat_q_norm", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, f32p, f32p,
 _sig("lvk_mul_mat_q_mfma", C.c_int, [C.c_int, u8p, C.c_int, C.c_int, C.c_void_p, f32p, C.c_int, f32p])
 _sig("lvk_attention", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p])
 _sig("lvk_attention_prompt", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p])
+_sig("lvk_attention_decode", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, f32p])
 _sig("lvk_attention_scores", C.c_int, [u16p, u16p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p, f32p])
 _sig("lvk_rms_norm_mul", C.c_int, [f32p, f32p, C.c_int, C.c_int, f32p])
 _sig("lvk_exp_table_mismatches", C.c_int, [])
@@ -287,6 +288,14 @@ def attention_prompt(kc, vc, q, n_embd, n_head, n_ctx, n_past, n):
     out = np.zeros(n * n_embd, np.float32)
     _check(lib.lvk_attention_prompt(kc, vc, np.ascontiguousarray(q, np.float32), n_embd, n_head, n_ctx, n_past, n, out),
            "lvk_attention_prompt")
+    return out
+
+
+def attention_decode(kc, vc, q, n_embd, n_head, n_ctx, n_past):
+    """the single-token attention kernels (lvk_attention_decode)"""
+    out = np.zeros(n_embd, np.float32)
+    _check(lib.lvk_attention_decode(kc, vc, np.ascontiguousarray(q, np.float32), n_embd, n_head, n_ctx, n_past, out),
+           "lvk_attention_decode")
     return out
 
 

@@ -138,6 +138,25 @@ def test_attention_prompt_kernels(lvk, oracle, monkeypatch, exp_path, n_past, N,
     assert np.array_equal(bits(got), bits(want))
 
 
+@pytest.mark.parametrize("exp_path", ["computed", "table"])
+@pytest.mark.parametrize("n_past,C,qs", [(0, 256, 1), (5, 256, 1), (31, 256, 1), (32, 256, 1), (63, 256, 8),
+                                         (64, 256, 1), (200, 256, 1), (255, 256, 4), (511, 512, 1), (700, 1024, 1),
+                                         (1000, 1024, 8), (2047, 2048, 1)])
+def test_attention_decode_kernels(lvk, oracle, monkeypatch, exp_path, n_past, C, qs):
+    """the split single-token attention (attention_decode.hip) is bit-identical to the reference graph"""
+    if exp_path == "table":
+        monkeypatch.setenv("LVK_EXP_TABLE", "1")
+    E, H = 512, 4
+    rng = np.random.default_rng(n_past * 7 + C)
+    kc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
+    vc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
+    q = (qs * rng.standard_normal(E)).astype(np.float32)
+    got = lvk.attention_decode(kc, vc, q, E, H, C, n_past)
+    want = np.zeros(E, np.float32)
+    oracle.lib.orc_attention(kc, vc, q, E, H, C, n_past, 1, want)
+    assert np.array_equal(bits(got), bits(want))
+
+
 def test_rms_norm_mul(lvk, oracle):
     rng = np.random.default_rng(3)
     x = (rng.standard_normal((4, 4096)) * 3).astype(np.float32)

@@ -4,13 +4,25 @@
 // Build: make -C tools/probe ; run on the GPU box.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
 #include "lvk_kernels.h"
+#include <cmath>
+#include <vector>
+// this host's fp16 exp table (as lvk_context.cpp host_fp16_tables: glibc expf, RNE to fp16)
+static void probe_exp_table(std::vector<uint16_t> & te) {
+    te.resize(65536);
+    for (int i = 0; i < 65536; ++i) {
+        uint16_t hi = (uint16_t) i; _Float16 hf; memcpy(&hf, &hi, 2);
+        const _Float16 e = (_Float16) expf((float) hf);
+        memcpy(&te[i], &e, 2);
+    }
+}
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1);} } while (0)
 using namespace lvk;
 #ifdef LVK_PROBE_TIMING
-namespace lvk { void * lvk_probe_trace(); void * lvk_probe_atrace(); }
+namespace lvk { void * lvk_probe_trace(); void * lvk_probe_atrace(); void * lvk_probe_dtrace(); }
 #endif
 
 __global__ void k_fill_u32(uint32_t * p, size_t n, uint32_t seed) {
@@ -90,8 +102,22 @@ int main(int argc, char ** argv) {
     StepParams * sp = (StepParams *) dalloc(16); CK(hipMemcpy(sp, &sph, 16, hipMemcpyHostToDevice));
     CK(hipDeviceSynchronize());
     hipStream_t s; CK(hipStreamCreate(&s));
+    int exp_mode = 1;
+    {
+        // the exp mode a context would pick (checked against this host's table)
+        std::vector<uint16_t> te;
+        probe_exp_table(te);
+        uint16_t * tb = (uint16_t *) dalloc(65536 * 2);
+        CK(hipMemcpy(tb, te.data(), 65536 * 2, hipMemcpyHostToDevice));
+        int * bad_d = (int *) dalloc(8); int bad[2];
+        CK(exp_check(tb, bad_d, 0)); CK(hipMemcpy(bad, bad_d, 8, hipMemcpyDeviceToHost));
+        exp_mode = getenv("LVK_EXP_TABLE") ? 0 : bad[1] == 0 ? 2 : bad[0] == 0 ? 1 : 0;
+        printf("exp check: double %d f32 %d mismatches -> mode %d\n", bad[0], bad[1], exp_mode);
+    }
 
     float * u = (float *) dalloc(F * 4); fill_f32(u, F, -1.f, 1.f, 18);
+    void * gran = dalloc(attention_decode_scratch_bytes(H, C));
+    CK(hipMemset(gran, 0, attention_decode_scratch_bytes(H, C)));
     const bool cu = getenv("LVK_PROBE_GENERIC") == nullptr;
     auto mv = [&](const MvLaunch & L, int pro, int epi) {
         if (cu) { hipError_t e = launch_matvec_cu(L, pro, epi, s); if (e != hipErrorNotSupported) return e; }
@@ -105,8 +131,9 @@ int main(int argc, char ** argv) {
             CK(mv(a, PRO_NORM, EPI_QKV));
         } else if (k == 1) {
             AttnLaunch at{q16, kc + (size_t) l * C * E, vc + (size_t) l * C * E, scores, aqa, Q4_0, etab, sp, 1, E, H, C};
-            at.exp_computed = getenv("LVK_EXP_TABLE") ? 0 : 1;   // timing only: random table
-            CK(launch_attention(at, s));
+            at.exp_computed = exp_mode;   // timing only: random table, mode of the real table check
+            if (getenv("LVK_ATTN_V1")) CK(launch_attention(at, s));
+            else CK(launch_attention_decode(at, gran, (unsigned) l + 1, s));
         } else if (k == 2) {
             MvLaunch b; b.w = y.wo; b.xq = aqa; b.y = x; b.sp = sp; b.n_tokens = 1;
             CK(mv(b, PRO_ACTQ, EPI_RESID));
@@ -138,6 +165,7 @@ int main(int argc, char ** argv) {
         hipLaunchKernelGGL(k_prefetch<8>, dim3(pf), dim3(pft), 0, s2, (const uint4 *) q.scl, sb, pfo);
     };
     CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    CK(hipMemsetAsync(gran, 0, attention_decode_scratch_bytes(H, C), s));   // per token (as the context)
     for (int l = 0; l < L; l++) {
         for (int k = 0; k < 5; k++) {
             op(k, l);
@@ -166,6 +194,7 @@ int main(int argc, char ** argv) {
         hipGraph_t g2; hipGraphExec_t ge2;
         int n = k < 5 ? L : 8;
         CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+        if (k == 1) CK(hipMemsetAsync(gran, 0, attention_decode_scratch_bytes(H, C), s));
         for (int l = 0; l < n; l++) op(k, l);
         CK(hipStreamEndCapture(s, &g2));
         CK(hipGraphInstantiate(&ge2, g2, nullptr, nullptr, 0));
@@ -181,6 +210,32 @@ int main(int argc, char ** argv) {
 #ifdef LVK_PROBE_TIMING
     {
         const int kind = getenv("LVK_TRACE_KIND") ? atoi(getenv("LVK_TRACE_KIND")) : 5;
+        if (kind == 1 && !getenv("LVK_ATTN_V1")) {
+            void * at = lvk_probe_dtrace();
+            std::vector<unsigned long long> h(32 * 4 * 4 * 8);
+            for (int l = 0; l < 4; l++) op(1, l);
+            CK(hipStreamSynchronize(s));
+            CK(hipMemset(gran, 0, attention_decode_scratch_bytes(H, C)));
+            CK(hipMemset(at, 0, h.size() * 8));
+            op(1, 4);
+            CK(hipStreamSynchronize(s));
+            CK(hipMemcpy(h.data(), at, h.size() * 8, hipMemcpyDeviceToHost));
+            double acc[8] = {0}; int n = 0;
+            unsigned long long t0min = ~0ull;
+            for (int w = 0; w < 32 * 4 * 4; w++) if (h[w * 8]) t0min = std::min(t0min, h[w * 8]);
+            double start_sp = 0;
+            for (int w = 0; w < 32 * 4 * 4; w++) {
+                unsigned long long * e = &h[(size_t) w * 8];
+                if (!e[0] || !e[5]) continue;
+                n++;
+                start_sp += (double) (e[0] - t0min);
+                for (int k = 1; k < 7; k++) acc[k] += (double) (e[k] - e[0]);
+            }
+            double a7 = 0; for (int w = 0; w < 32 * 4 * 4; w++) { unsigned long long * e = &h[(size_t) w * 8]; if (e[0] && e[5]) a7 += (double) (e[7] - e[0]); }
+            printf("decode attention trace (%d waves): qk-issued %.0f  v0-dma %.0f  sp+dma-issued %.0f  scores %.0f  exchange %.0f  softmax %.0f  dma-wait %.0f cycles\n",
+                   n, acc[6] / n, a7 / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+            return 0;
+        }
         if (kind == 1) {
             void * at = lvk_probe_atrace();
             std::vector<unsigned long long> h(64 * 64);
