@@ -34,6 +34,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 MODEL_BYTES_7B = 4130490880    # algorithmic weight bytes per token
 MODEL_BYTES_13B_Q41 = 9640369920   # 13B Q4_1 weight bytes per token
 REF_PUBLISHED_TOKS = 16.3      # 7B Q4_0 predict 61.41 ms/token
+LAYER_MAT_WEIGHTS_7B = 32 * (4 * 4096 * 4096 + 3 * 4096 * 11008)   # weights of the 7B layer matrices
+VALU_FP32_TFLOPS = 157.3       # MI355X_MICROARCH.md: peak FP32 vector
+INT8_DENSE_TOPS = 5000.0       # dense INT8/FP8 matrix-core peak (no 2:1 sparsity)
 
 
 def prompt_tokens(n):
@@ -231,8 +234,25 @@ def main():
         m.eval(p512, 0)
         best = min(best, time.perf_counter() - t0)
     best = all_max(pg, best)
+    # the bit-faithful floor is the reference's fp32 chains -- one fmaf per
+    # 4-element integer partial -- at the VALU FP32 peak; the INT8 line prices the same
+    # matmul MACs on the dense matrix-core peak (what a non-faithful GEMM could reach)
+    fmas = 512 * LAYER_MAT_WEIGHTS_7B / 4
+    macs = 512 * LAYER_MAT_WEIGHTS_7B
     prompt = {"value": n_gpus * 512 / best, "unit": "tok/s", "n_tokens": 512, "ms": best * 1e3,
-              "path": "bit-faithful VALU (v_dot8_i32_i4 + fp32 FMA chains)"}
+              "path": "matrix cores (v_mfma_f32_32x32x8_f16 exact 4-element integer partials, f32 MFMA scale "
+                      "products) + VALU fp32 chains; bit-identical to the AVX2 reference",
+              "roofline": {"bound": "valu-fp32 (the reference's sequential fp32 FMA chains)",
+                           "achieved": 2 * fmas / best / 1e12, "peak": VALU_FP32_TFLOPS, "unit": "TFLOP/s",
+                           "frac": 2 * fmas / best / 1e12 / VALU_FP32_TFLOPS, "fp32_chain_fmas": fmas},
+              "int8_mfma_equiv": {"ops": 2 * macs, "achieved_tops": 2 * macs / best / 1e12,
+                                  "peak_tops": INT8_DENSE_TOPS, "frac": 2 * macs / best / 1e12 / INT8_DENSE_TOPS}}
+    m.set_profiling(True)
+    m.reset_profile()
+    m.eval(p512, 0)
+    pp = m.profile()
+    m.set_profiling(False)
+    prompt["kernels_ms"] = {k: v["ms"] for k, v in pp.items() if v["launches"]}
 
     # profiled decode pass: HIP events around every kernel class
     m.set_profiling(True)

@@ -5,7 +5,7 @@
 //
 // A decode step reads 2 * n_kv * 256 B of K and V per head; one workgroup per
 // head pulls ~100 KB through one CU at ~17 B/cycle.  Here 4 workgroups share a
-// head, grid (H, 4):
+// head:
 //   1. workgroup (h, s) DMAs the V rows of its 32-dim slice (one weight block
 //      of the merged heads) into LDS, and scores the positions of 64-position
 //      chunks s, s+4, ... (a lane quad per position): KQ = ggml_vec_dot_f16
@@ -19,11 +19,26 @@
 //      P.V with the AVX accumulator layout (a quad per dim) and the double
 //      tail past n_kv & ~31 (ggml.c:1806-1808); the slice is quantized to the
 //      Wo weight format (quantize_row_q4_0 / _q4_1, ggml.c:621-685 / 847-920).
-// All 4*H workgroups are co-resident (grid <= CUs), which the exchange needs;
-// the spin is bounded so a violated assumption cannot hang the GPU.
+//
+// k_attn_wo runs the same attention and the Wo matvec + residual add
+// (llama.cpp:1064-1071) in ONE launch.  The first workgroups of its grid are
+// Wo workgroups laid out like matvec_cu.hip (one per CU, contiguous row
+// groups, a wave per row group): each wave puts its whole first row group in
+// flight at launch, then takes the attention output -- the Q4_0 blocks of the
+// merged heads -- from 5 granules per block that the attention workgroups
+// publish (same R2 form), builds its activation table and finishes its rows.
+// That removes the launch boundary between attention and Wo and hides Wo's
+// weight stream behind the attention.
+//
+// Every workgroup of a launch is resident at once (the host checks it), which
+// the exchanges need; every spin is bounded so a violated assumption cannot
+// hang the GPU.
 #include "lvk_device.h"
 #include "lvk_kernels.h"
 #include "matvec_common.h"
+
+#include <algorithm>
+#include <type_traits>
 
 namespace lvk {
 
@@ -55,40 +70,65 @@ __device__ __forceinline__ float quad_reduce(const float s[8]) {
 }
 
 typedef unsigned long long u64g __attribute__((address_space(1)));
+typedef unsigned u32g __attribute__((address_space(1)));
+
+// relaxed agent-scope poll of one granule until it carries `epoch`; bounded so a
+// violated residency assumption ends in wrong numbers, never in a hung GPU
+__device__ __forceinline__ unsigned long long poll_granule(u64g * p, unsigned epoch) {
+    unsigned long long x;
+    for (int spins = 0;; ++spins) {
+        x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned) (x >> 32) == epoch || spins > (1 << 22)) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return x;
+}
 
 #ifdef LVK_PROBE_TIMING   // dev probe builds only: per-wave s_memtime phase stamps
 __device__ unsigned long long g_dtrace[32 * 4 * 4 * 8];
 #define LVK_DT(ev)                                                                                       \
     do {                                                                                                 \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                      \
-        if ((threadIdx.x & 63) == 0) g_dtrace[((blockIdx.x * 4 + blockIdx.y) * 4 + (threadIdx.x >> 6)) * 8 + (ev)] = t_; \
+        if ((threadIdx.x & 63) == 0 && h < 32) g_dtrace[((h * 4 + sl) * 4 + (threadIdx.x >> 6)) * 8 + (ev)] = t_; \
     } while (0)
 #else
 #define LVK_DT(ev) do { } while (0)
 #endif
 
+struct AttnDArgs {
+    const uint16_t * q16;
+    const uint16_t * kc;
+    const uint16_t * vc;
+    unsigned long long * gran;    // [H][n_ctx] score granules
+    unsigned long long * ogran;   // k_attn_wo: [E/32][5] output granules; nullptr: write `out`
+    unsigned * ocount;            // k_attn_wo: attention workgroups done, + 4H per layer
+    const uint16_t * exp_tab;
+    const StepParams * sp;
+    int E, n_ctx;
+    float scale;
+    unsigned epoch;
+    ActQ out;
+    float * out_f32;
+    int exp_mode;
+};
+
 template <int QT>
-__global__ __launch_bounds__(256) void k_attn_d(const uint16_t * __restrict__ q16, const uint16_t * __restrict__ kc,
-                                                const uint16_t * __restrict__ vc, unsigned long long * gran,
-                                                const uint16_t * __restrict__ exp_tab, const StepParams * sp, int E,
-                                                int n_ctx, float scale, unsigned epoch, ActQ out,
-                                                float * __restrict__ out_f32, int exp_mode) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int h = blockIdx.x, sl = blockIdx.y, d0 = h * HD + sl * 32;
+__device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, const int sl, uint8_t * smem) {
+    const int E = A.E, n_ctx = A.n_ctx, d0 = h * HD + sl * 32;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = tid & 3;
     uint16_t * vl = (uint16_t *) smem;                           // [32 dims][n_ctx]
     float * sc = (float *) (smem + (size_t) 32 * n_ctx * 2);     // [n_ctx]
     uint16_t * pl = (uint16_t *) (sc + n_ctx);                   // [n_ctx]
     float * red = (float *) (pl + n_ctx);                        // 8 floats
     double * redd = (double *) (red + 8);                        // 4 doubles
-    u64g * g = (u64g *) (gran + (size_t) h * n_ctx);
+    u64g * g = (u64g *) (A.gran + (size_t) h * n_ctx);
     LVK_DT(0);
 
     // 1a. loads that do not depend on n_past go out before the step block is read (its
     // load is a full memory round trip): Q, the K rows of this workgroup's first two
     // 64-position chunks and the first 512 positions of its 32 V rows (addresses inside
     // the caches; positions past n_kv are never used)
-    const uint4 * qp = (const uint4 *) (q16 + h * HD) + r;
+    const uint4 * qp = (const uint4 *) (A.q16 + h * HD) + r;
     uint4 qv[4];
 #pragma unroll
     for (int st = 0; st < 4; ++st) qv[st] = qp[st * 4];
@@ -96,21 +136,21 @@ __global__ __launch_bounds__(256) void k_attn_d(const uint16_t * __restrict__ q1
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const int p = min(sl * 64 + c * 256 + (tid >> 2), n_ctx - 1);
-        const uint4 * kp = (const uint4 *) (kc + (size_t) p * E + h * HD) + r;
+        const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
 #pragma unroll
         for (int st = 0; st < 4; ++st) kv[c][st] = kp[st * 4];
     }
     auto v_dma = [&](int p0, int lim) {             // positions [p0, p0 + 512) of the 32 rows, below lim
         for (int row = wave; row < 32; row += 4)
             if (p0 + lane * 8 < lim)
-                __builtin_amdgcn_global_load_lds((const void *) (vc + (size_t) (d0 + row) * n_ctx + p0 + lane * 8),
+                __builtin_amdgcn_global_load_lds((const void *) (A.vc + (size_t) (d0 + row) * n_ctx + p0 + lane * 8),
                                                  (__attribute__((address_space(3))) void *) (vl + (size_t) row * n_ctx + p0),
                                                  16, 0, 0);
     };
     LVK_DT(6);
     v_dma(0, min(n_ctx, 512));
     LVK_DT(7);
-    const int n_kv = sp->n_past + 1;
+    const int n_kv = A.sp->n_past + 1;
     const int n_pad = (n_kv + 31) & ~31;
     const int np = n_kv & ~31;
     for (int p0 = 512; p0 < n_pad; p0 += 512) v_dma(p0, n_pad);
@@ -132,8 +172,8 @@ __global__ __launch_bounds__(256) void k_attn_d(const uint16_t * __restrict__ q1
             }
             const float kq = quad_reduce(s);
             if (r == 0 && p < n_kv) {
-                const float v = kq * scale;                      // ggml_vec_scale_f32 (llama.cpp:1026)
-                __hip_atomic_store(g + p, ((unsigned long long) epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                const float v = kq * A.scale;                    // ggml_vec_scale_f32 (llama.cpp:1026)
+                __hip_atomic_store(g + p, ((unsigned long long) A.epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
         };
@@ -142,7 +182,7 @@ __global__ __launch_bounds__(256) void k_attn_d(const uint16_t * __restrict__ q1
             if (sl * 64 + c * 256 < n_kv) score(kv[c], sl * 64 + c * 256 + (tid >> 2));
         for (int c0 = sl * 64 + 512; c0 < n_kv; c0 += 256) {
             const int p = c0 + (tid >> 2);
-            const uint4 * kp = (const uint4 *) (kc + (size_t) min(p, n_kv - 1) * E + h * HD) + r;
+            const uint4 * kp = (const uint4 *) (A.kc + (size_t) min(p, n_kv - 1) * E + h * HD) + r;
             uint4 k4[4];
 #pragma unroll
             for (int st = 0; st < 4; ++st) k4[st] = kp[st * 4];
@@ -153,13 +193,7 @@ __global__ __launch_bounds__(256) void k_attn_d(const uint16_t * __restrict__ q1
     // 2. every score of the head: poll each granule until it carries this layer's epoch
     float mx = -INFINITY;
     for (int p = tid; p < n_kv; p += 256) {
-        unsigned long long x;
-        for (int spins = 0;; ++spins) {
-            x = __hip_atomic_load(g + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned) (x >> 32) == epoch || spins > (1 << 22)) break;      // bounded: never hang
-            __builtin_amdgcn_s_sleep(1);
-        }
-        const float v = __uint_as_float((unsigned) x);
+        const float v = __uint_as_float((unsigned) poll_granule(g + p, A.epoch));
         sc[p] = v;
         mx = v > mx ? v : mx;
     }
@@ -174,7 +208,7 @@ __global__ __launch_bounds__(256) void k_attn_d(const uint16_t * __restrict__ q1
     // softmax (ggml.c:7099-7121): no position is masked in a decode step
     double sum = 0.0;    // exact in any order: every term is an fp16 value in [0,1]
     for (int p = tid; p < n_kv; p += 256) {
-        const float e = f16_to_f32(exp_f16(f32_to_f16(sc[p] - mx), exp_tab, exp_mode));
+        const float e = f16_to_f32(exp_f16(f32_to_f16(sc[p] - mx), A.exp_tab, A.exp_mode));
         sum += (double) e;
         sc[p] = e;
     }
@@ -233,7 +267,7 @@ __global__ __launch_bounds__(256) void k_attn_d(const uint16_t * __restrict__ q1
     __syncthreads();
     if (tid < 32) {
         const float v = ob[tid];
-        if (out_f32) out_f32[d0 + tid] = v;
+        if (A.out_f32) A.out_f32[d0 + tid] = v;
         const int blk = d0 / 32;
         if constexpr (QT == Q4_0) {
             float amax = fabsf(v);
@@ -246,9 +280,22 @@ __global__ __launch_bounds__(256) void k_attn_d(const uint16_t * __restrict__ q1
             part |= __shfl_xor(part, 2);
             part |= __shfl_xor(part, 4);
             const uint32_t w0 = __shfl(part, 0), w1 = __shfl(part, 8), w2 = __shfl(part, 16), w3 = __shfl(part, 24);
-            if (tid == 0) {
-                out.d[blk] = dd;
-                out.qs[blk] = make_uint4(w0, w1, w2, w3);
+            if (A.ogran) {
+                // k_attn_wo: the block goes to the Wo workgroups as 5 granules {epoch, d | qs word}
+                if (tid < 5) {
+                    const uint32_t wv = tid == 0 ? __float_as_uint(dd) : tid == 1 ? w0 : tid == 2 ? w1 : tid == 3 ? w2 : w3;
+                    __hip_atomic_store((u64g *) A.ogran + (size_t) blk * 5 + tid, ((unsigned long long) A.epoch << 32) | wv,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                // then one lane counts this workgroup in (the storing wave drained first:
+                // MI355X_MICROARCH.md, valid hand-off forms, row 1); the Wo waves poll only
+                // that counter -- 512 waves polling 640 granules each would eat the chip's
+                // bandwidth the attention itself needs
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (tid == 0) __hip_atomic_fetch_add((u32g *) A.ocount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (tid == 0) {
+                A.out.d[blk] = dd;
+                A.out.qs[blk] = make_uint4(w0, w1, w2, w3);
             }
         }
     }
@@ -259,13 +306,195 @@ __global__ __launch_bounds__(256) void k_attn_d(const uint16_t * __restrict__ q1
             float dd, mm;
             uint32_t qw;
             mv::q41_block_lds(ob, tid, dd, mm, qw);
-            ((uint32_t *) (out.qs + blk))[tid] = qw;
+            ((uint32_t *) (A.out.qs + blk))[tid] = qw;
             if (tid == 0) {
-                out.d[blk] = dd;
-                out.m[blk] = mm;
+                A.out.d[blk] = dd;
+                A.out.m[blk] = mm;
             }
         }
     }
+}
+
+template <int QT>
+__global__ __launch_bounds__(256) void k_attn_d(AttnDArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    attn_d_run<QT>(A, blockIdx.x, blockIdx.y, smem);
+}
+
+// ---- k_attn_wo: the Wo workgroups (row length n_embd = 4096 compiled in) ----
+namespace wo {
+constexpr int KT = 4096;
+constexpr int NB = KT / 32;        // blocks per row
+constexpr int NC = NB / 32;        // chunks of 32 blocks (4 x uint4 + 1 float4 per lane each)
+constexpr int NW = 4;              // waves per Wo workgroup
+constexpr int D = NC;              // a whole row group in flight
+constexpr int LDS_WAVE = NB * 32 + NC * 128 + 2 * 256 * 4;   // activation table | dx | s staging
+}  // namespace wo
+
+struct WoArgs {
+    const uint4 * nib;
+    const float4 * scl;
+    int G;          // row groups (M / 8)
+    float * y;      // residual stream: y[row] += (Wo x)[row] (llama.cpp:1071)
+    int nwg;        // Wo workgroups = the first nwg of the grid
+};
+
+__device__ __forceinline__ void wo_run(const WoArgs & P, unsigned long long * ogran, unsigned * ocount,
+                                       const unsigned target, const unsigned epoch, const int b, uint8_t * smem) {
+    using namespace wo;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 7, r = lane >> 3;
+    const int g0 = (int) ((unsigned) b * (unsigned) P.G / (unsigned) P.nwg);
+    const int g1 = (int) ((unsigned) (b + 1) * (unsigned) P.G / (unsigned) P.nwg);
+    const int ng = (g1 - g0 - wave + NW - 1) / NW;       // row groups of this wave
+    if (ng <= 0) return;
+    int gc = g0 + wave;
+
+    // 1. the wave's first row group in flight before anything waits (matvec_cu.hip image
+    // and load form: wave-uniform base + 32-bit lane offset, nt policy)
+    const uint32_t loff = (uint32_t) lane * 16u;
+    uint4 W[D][4];
+    float4 S[D];
+#define LVK_WO_ISSUE(slot, grp, cc)                                                                      \
+    do {                                                                                                 \
+        const uint4 * nb_ = P.nib + ((size_t) (grp) * NC * 4 + (cc) * 4) * 64;                           \
+        _Pragma("unroll") for (int sb = 0; sb < 4; ++sb)                                                 \
+            W[slot][sb] = ld_nt((const uint4 *) ((const char *) (nb_ + sb * 64) + loff));                \
+        S[slot] = *(const float4 *) ((const char *) (P.scl + ((size_t) (grp) * NC + (cc)) * 64) + loff); \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+    } while (0)
+#pragma unroll
+    for (int d = 0; d < D; ++d) LVK_WO_ISSUE(d, gc, d);
+
+    // 2. the Wo input: 5 granules per block from the attention workgroups, into this
+    // wave's own activation table (matvec_common.h layout)
+    uint32_t * act = (uint32_t *) (smem + (size_t) wave * LDS_WAVE);
+    float * dxp = (float *) (smem + (size_t) wave * LDS_WAVE + NB * 32);
+    float * sw = dxp + NC * 32;
+    // one lane waits for every attention workgroup's count (a single word, slow poll),
+    // then the wave reads the 640 granules once; a tag that is not yet this layer's is
+    // polled again (not expected after the count)
+    if (lane == 0) {
+        // the attention takes several microseconds: sleep through most of it before the
+        // first poll, then poll sparsely (hundreds of pollers on one word cost the chip)
+        __builtin_amdgcn_s_sleep(127);
+        __builtin_amdgcn_s_sleep(127);
+        for (int spins = 0; __hip_atomic_load((u32g *) ocount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+                            spins < (1 << 20);
+             ++spins)
+            __builtin_amdgcn_s_sleep(16);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");     // no granule load above the wait
+    u64g * og = (u64g *) ogran;
+    static_assert(NB * 5 == 10 * 64, "granules per lane");
+    unsigned long long gv[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) gv[k] = __hip_atomic_load(og + lane + 64 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        const int i = lane + 64 * k;
+        const unsigned word = (unsigned) ((unsigned) (gv[k] >> 32) == epoch ? gv[k] : poll_granule(og + i, epoch));
+        const int blk = i / 5, k5 = i - blk * 5;
+        if (k5 == 0) dxp[(blk >> 5) * 32 + (blk & 7) * 4 + ((blk >> 3) & 3)] = __uint_as_float(word);
+        else mv::act_store(act, dxp, blk, k5 - 1, word, 0.0f, false);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // other lanes of this wave read the table
+
+    // 3. the rows: ggml_vec_dot_q4_0 AVX2 chains (ggml.c:1950-2026) as in matvec_cu.hip
+    auto body = [&](auto has_next, int gnext) __attribute__((always_inline)) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            float * sl = sw + (c & 1) * 256;
+            // s = dw * dx of blocks 32c + 8m + j of row r (ggml.c:1968)
+            const float4 dx = *(const float4 *) (dxp + c * 32 + j * 4);
+            float4 sv;
+            sv.x = S[c].x * dx.x; sv.y = S[c].y * dx.y; sv.z = S[c].z * dx.z; sv.w = S[c].w * dx.w;
+            *(float4 *) (sl + r * 32 + j * 4) = sv;
+            __builtin_amdgcn_wave_barrier();
+            float sa[8][4];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const float4 v = *(const float4 *) (sl + r * 32 + jj * 4);
+                sa[jj][0] = v.x; sa[jj][1] = v.y; sa[jj][2] = v.z; sa[jj][3] = v.w;
+            }
+#pragma unroll
+            for (int sb = 0; sb < 4; ++sb) {
+                const uint32_t wd[4] = {W[c][sb].x, W[c][sb].y, W[c][sb].z, W[c][sb].w};
+#pragma unroll
+                for (int pp = 0; pp < 2; ++pp) {
+                    const int bi = sb * 8 + pp * 4;
+                    const uint4 a = *(const uint4 *) (act + ((c * 8 + sb * 2 + pp) * 8 + j) * 4);
+                    const int p0 = dot8(wd[2 * pp], a.x);
+                    const int p1 = dot8(wd[2 * pp], a.y);
+                    const int p2 = dot8(wd[2 * pp + 1], a.z);
+                    const int p3 = dot8(wd[2 * pp + 1], a.w);
+                    acc = __builtin_fmaf(sa[(bi + 0) & 7][(bi + 0) >> 3], (float) p0, acc);
+                    acc = __builtin_fmaf(sa[(bi + 1) & 7][(bi + 1) >> 3], (float) p1, acc);
+                    acc = __builtin_fmaf(sa[(bi + 2) & 7][(bi + 2) >> 3], (float) p2, acc);
+                    acc = __builtin_fmaf(sa[(bi + 3) & 7][(bi + 3) >> 3], (float) p3, acc);
+                }
+            }
+            // this slot is free: the same chunk of the wave's next row group
+            if constexpr (decltype(has_next)::value) LVK_WO_ISSUE(c, gnext, c);
+            asm volatile("" : "+v"(acc));     // chunks in program order (matvec_cu.hip rule 4)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return mv::octet_reduce(acc);
+    };
+    for (int k = 0; k + 1 < ng; ++k) {
+        const float res = body(std::true_type{}, gc + NW);
+        if (j == 0) P.y[gc * 8 + r] = res + P.y[gc * 8 + r];       // ggml_add(cur, inpSA) (llama.cpp:1071)
+        gc += NW;
+    }
+    const float res = body(std::false_type{}, gc);
+    if (j == 0) P.y[gc * 8 + r] = res + P.y[gc * 8 + r];
+#undef LVK_WO_ISSUE
+}
+
+__global__ __launch_bounds__(256) void k_attn_wo(AttnDArgs A, WoArgs P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int b = blockIdx.x;
+    // attention workgroups first (dispatched first, one per CU on half the chip; the 4
+    // slices of a head on one XCD as in k_attn_d's (H, 4) grid), then the Wo workgroups
+    const int nattn = (int) gridDim.x - P.nwg;
+    if (b < nattn) attn_d_run<Q4_0>(A, (b & 7) + 8 * (b >> 5), (b >> 3) & 3, smem);
+    else wo_run(P, A.ogran, A.ocount, (unsigned) nattn * A.epoch, A.epoch, b - nattn, smem);
+}
+
+int n_cus() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, v = 0;
+        n = (hipGetDevice(&dev) == hipSuccess &&
+             hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+                ? v
+                : 256;
+    }
+    return n;
+}
+
+size_t attn_lds(int n_ctx) { return (size_t) 32 * n_ctx * 2 + (size_t) n_ctx * 6 + 64; }
+
+AttnDArgs attn_args(const AttnLaunch & A, void * gran, unsigned epoch) {
+    AttnDArgs a{};
+    a.q16 = A.q16;
+    a.kc = A.kc;
+    a.vc = A.vc;
+    a.gran = (unsigned long long *) gran;
+    a.ogran = nullptr;
+    a.ocount = nullptr;
+    a.exp_tab = A.exp_tab;
+    a.sp = A.sp;
+    a.E = A.n_embd;
+    a.n_ctx = A.n_ctx;
+    a.scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
+    a.epoch = epoch;
+    a.out = A.out;
+    a.out_f32 = A.out_f32;
+    a.exp_mode = A.exp_computed;
+    return a;
 }
 
 }  // namespace
@@ -278,22 +507,44 @@ bool attention_decode_supported(int n_embd, int n_head, int n_ctx) {
     return n_embd / n_head == HD && n_ctx % 64 == 0 && n_ctx <= 2048 && n_head * 4 <= 1024;
 }
 
-size_t attention_decode_scratch_bytes(int n_head, int n_ctx) { return (size_t) n_head * n_ctx * 8; }
+size_t attention_decode_scratch_bytes(int n_head, int n_ctx) {
+    // score granules [H][n_ctx], then k_attn_wo's output granules [E/32][5] (room for 6)
+    return (size_t) n_head * n_ctx * 8 + (size_t) n_head * (HD / 32) * 6 * 8;
+}
 
 hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned epoch, hipStream_t s) {
     if (!attention_decode_supported(A.n_embd, A.n_head, A.n_ctx) || A.n_tokens != 1 || epoch == 0)
         return hipErrorNotSupported;
     if (A.out_qtype != Q4_0 && A.out_qtype != Q4_1) return hipErrorNotSupported;
-    const float scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
-    const size_t lds = (size_t) 32 * A.n_ctx * 2 + (size_t) A.n_ctx * 6 + 64;
+    const AttnDArgs a = attn_args(A, gran, epoch);
+    const size_t lds = attn_lds(A.n_ctx);
     if (A.out_qtype == Q4_1)
-        LVK_LAUNCH(k_attn_d<Q4_1>, dim3(A.n_head, HD / 32), dim3(256), lds, s, A.q16, A.kc, A.vc,
-                   (unsigned long long *) gran, A.exp_tab, A.sp, A.n_embd, A.n_ctx, scale, epoch, A.out, A.out_f32,
-                   A.exp_computed);
+        LVK_LAUNCH(k_attn_d<Q4_1>, dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
     else
-        LVK_LAUNCH(k_attn_d<Q4_0>, dim3(A.n_head, HD / 32), dim3(256), lds, s, A.q16, A.kc, A.vc,
-                   (unsigned long long *) gran, A.exp_tab, A.sp, A.n_embd, A.n_ctx, scale, epoch, A.out, A.out_f32,
-                   A.exp_computed);
+        LVK_LAUNCH(k_attn_d<Q4_0>, dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+bool attention_wo_supported(int n_embd, int n_head, int n_ctx, const QMatrix & w) {
+    if (!attention_decode_supported(n_embd, n_head, n_ctx)) return false;
+    if (n_embd != wo::KT || w.qtype != Q4_0 || w.K != wo::KT || w.M <= 0 || w.M % 8) return false;
+    // every workgroup resident at once: the Wo workgroups plus 4 per head at two per CU
+    const int nwg = std::min(n_cus(), w.M / 8);
+    const size_t lds = std::max(attn_lds(n_ctx), (size_t) wo::NW * wo::LDS_WAVE);
+    return n_head % 8 == 0 && nwg + 4 * n_head <= 2 * n_cus() && 2 * lds <= 160 * 1024;
+}
+
+hipError_t launch_attention_wo(const AttnLaunch & A, const QMatrix & w, float * y, void * gran, unsigned epoch,
+                               hipStream_t s) {
+    if (!attention_wo_supported(A.n_embd, A.n_head, A.n_ctx, w) || A.n_tokens != 1 || epoch == 0 ||
+        A.out_qtype != Q4_0 || !y)
+        return hipErrorNotSupported;
+    AttnDArgs a = attn_args(A, gran, epoch);
+    a.ogran = a.gran + (size_t) A.n_head * A.n_ctx;
+    a.ocount = (unsigned *) (a.ogran + (size_t) A.n_head * (HD / 32) * 5);   // inside the 6-per-block room
+    const WoArgs P{w.nib, (const float4 *) w.scl, w.M / 8, y, std::min(n_cus(), w.M / 8)};
+    const size_t lds = std::max(attn_lds(A.n_ctx), (size_t) wo::NW * wo::LDS_WAVE);
+    LVK_LAUNCH(k_attn_wo, dim3(P.nwg + 4 * A.n_head), dim3(256), lds, s, a, P);
     return hipGetLastError();
 }
 

@@ -152,6 +152,13 @@ hipError_t exp_check(const uint16_t * exp_tab, int * bad_d, hipStream_t s);
 bool attention_decode_supported(int n_embd, int n_head, int n_ctx);
 size_t attention_decode_scratch_bytes(int n_head, int n_ctx);
 hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned epoch, hipStream_t s);
+// the same attention + the Wo matvec + residual add (y += Wo attn) in ONE launch
+// (attention_decode.hip, k_attn_wo): Q4_0 Wo with K = 4096 and every workgroup
+// resident (n_ctx <= 1024 here); the attention output reaches the Wo workgroups
+// as tagged granules in `gran` (same scratch and zeroing as launch_attention_decode)
+bool attention_wo_supported(int n_embd, int n_head, int n_ctx, const QMatrix & wo);
+hipError_t launch_attention_wo(const AttnLaunch & A, const QMatrix & wo, float * y, void * gran, unsigned epoch,
+                               hipStream_t s);
 
 // one-time weight repack: file-layout rows (ggml blocks) -> quad-sliced image
 // interleave4: src_rows holds two (M/2)-row matrices A then B; the image

@@ -48,6 +48,7 @@ namespace {
 typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef float f32x32_t __attribute__((ext_vector_type(32)));
 
 constexpr int TM = 128;     // rows per workgroup
 constexpr int TN = 16;      // tokens per workgroup (one token tile)
@@ -223,31 +224,27 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
         if (scales_next) load_scales(ch + 1);
         const float * wl = (const float *) (smem + ((ch & 1) ? OFF_DW1 : OFF_DW0));
         const float * dl = (const float *) (smem + ((ch & 1) ? OFF_DA1 : OFF_DA0));
-        // this lane's dw (16 rows) and da for block jc of the chunk, read one block ahead
-        float4 d4[4];
-        float dav;
-        auto read_scales = [&](int jc) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (LVK_MM_EXP & 16) d4[q] = make_float4(jc, q, 1.f, 2.f);
-                else d4[q] = *(const float4 *) (wl + jc * DWS + 32 * w + 8 * q + 4 * h);
-            }
-            dav = (LVK_MM_EXP & 16) ? 1.5f : dl[jc * DAS + (lane & 15)];
-        };
-        read_scales((u & 3) * 8);
+        // the block scales s = dw * da (ggml.c:1968) of every (row, token) output come from
+        // the matrix core as an outer product, K = 1: each element is one rounded f32
+        // multiply, bit-identical to the VALU product.  v_mfma_f32_32x32x1f32 (2 blocks):
+        // lane half h feeds block jb + h (dw of row l&31, da of token (l&31)&15); block b
+        // lands in registers 16b..16b+15 in the standard 32x32 C/D layout, i.e. exactly the
+        // (rows, column) of the chain partials below.
+        f32x32_t SC;
 #pragma unroll
         for (int jb = 0; jb < 8; ++jb) {
             const int blk = 8 * u + jb;
             const uint32_t sel = (jb & 1) ? 0x0C030C02u : 0x0C010C00u;
             uint2 (&bf)[4] = bq[jb % PD];
-            // s = dw * da for this lane's 16 rows (ggml.c:1968)
+            if ((jb & 1) == 0) {
+                const int jc = (u & 3) * 8 + jb + h;        // block of the chunk this lane half feeds
+                const float dwa = wl[jc * DWS + 32 * w + rho];
+                const float dab = dl[jc * DAS + (lane & 15)];
+                SC = __builtin_amdgcn_mfma_f32_32x32x1f32(dwa, dab, (f32x32_t){}, 0, 0, 0);
+            }
             float sc[16];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                sc[4 * q + 0] = d4[q].x * dav; sc[4 * q + 1] = d4[q].y * dav;
-                sc[4 * q + 2] = d4[q].z * dav; sc[4 * q + 3] = d4[q].w * dav;
-            }
-            if (jb + 1 < 8) read_scales((u & 3) * 8 + jb + 1);     // in flight during this block's chains
+            for (int i = 0; i < 16; ++i) sc[i] = SC[16 * (jb & 1) + i];
             // software pipeline: the MFMA of chain pair c+1 is in flight while the VALU runs the
             // chains of pair c (ggml.c:2013: acc_j = fmaf(d, P_j, acc_j))
             f32x16_t Pc[2];

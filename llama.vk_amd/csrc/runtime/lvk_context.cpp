@@ -101,6 +101,7 @@ void Context::init(const llama_context_params & p) {
         uf = (float *) model.alloc(C * F * 4);
         prompt_exact = getenv("LVK_PROMPT_EXACT") && atoi(getenv("LVK_PROMPT_EXACT")) != 0;
         old_attention = getenv("LVK_ATTN_V1") && atoi(getenv("LVK_ATTN_V1")) != 0;
+        fuse_attn_wo = getenv("LVK_FUSE_ATTN_WO") && atoi(getenv("LVK_FUSE_ATTN_WO")) != 0;
         attn_gran = model.alloc(attention_decode_scratch_bytes((int) H, (int) C));
     }
     logits_d = (float *) model.alloc(C * V * 4);
@@ -253,6 +254,9 @@ void Context::enqueue_forward(int n, bool last_only) {
     }
     // single-token FFN: W1|W3 hands silu(w1 x)*(w3 x) to W2 in f32, W2 quantizes it
     const bool ffn_f32 = n == 1 && model.qtype == Q4_0 && matvec_cu_supported(E) && matvec_cu_supported(F);
+    // attention, Wo and the residual add in one launch (attention_decode.hip, k_attn_wo)
+    const bool attn_wo = n == 1 && !old_attention && fuse_attn_wo && model.qtype == Q4_0 && !model.layers.empty() &&
+                         attention_wo_supported(E, H, n_ctx, model.layers[0].wo);
     if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx))
         // the decode attention's score granules carry epoch = layer + 1: zero them once per token
         LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes(H, n_ctx), stream));
@@ -267,15 +271,23 @@ void Context::enqueue_forward(int n, bool last_only) {
         timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
         AttnLaunch at{q16, kc + il * CE, vc + il * CE, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
         at.exp_computed = exp_computed;
-        if (n > 1 && model.qtype == Q4_0 && attention_prompt_supported(E, H, n_ctx))
-            timed_launch(K_ATTN, 0, [&] { return launch_attention_prompt(at, (uint16_t *) scores, nullptr, nullptr, stream); });
-        else if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx))
-            timed_launch(K_ATTN, 0, [&] { return launch_attention_decode(at, attn_gran, (unsigned) il + 1, stream); });
-        else
-            timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
-        MvLaunch b;
-        b.w = ly.wo; b.xq = aq_attn; b.y = x; b.sp = sp_d; b.n_tokens = n;
-        timed_launch(K_WO, qbytes(ly.wo), [&] { return mv_launch(b, PRO_ACTQ, EPI_RESID, stream); });
+        if (attn_wo) {
+            timed_launch(K_ATTN_WO, qbytes(ly.wo), [&] {
+                return launch_attention_wo(at, ly.wo, x, attn_gran, (unsigned) il + 1, stream);
+            });
+        } else {
+            if (n > 1 && model.qtype == Q4_0 && attention_prompt_supported(E, H, n_ctx))
+                timed_launch(K_ATTN, 0, [&] {
+                    return launch_attention_prompt(at, (uint16_t *) scores, nullptr, nullptr, stream);
+                });
+            else if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx))
+                timed_launch(K_ATTN, 0, [&] { return launch_attention_decode(at, attn_gran, (unsigned) il + 1, stream); });
+            else
+                timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
+            MvLaunch b;
+            b.w = ly.wo; b.xq = aq_attn; b.y = x; b.sp = sp_d; b.n_tokens = n;
+            timed_launch(K_WO, qbytes(ly.wo), [&] { return mv_launch(b, PRO_ACTQ, EPI_RESID, stream); });
+        }
         MvLaunch c;
         c.w = ly.w13; c.x = x; c.g = ly.ffn_norm; c.sp = sp_d; c.n_tokens = n; c.silu_tab = silu_tab;
         c.out_q = aq_ffn; c.u = u_ffn;

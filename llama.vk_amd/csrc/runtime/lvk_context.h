@@ -12,7 +12,7 @@ struct llama_context_params;
 namespace lvk {
 
 // kernel classes timed by the profiler (events around every launch of a class)
-enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_WO, K_W13, K_W2, K_LMHEAD, K_NCLASS };
+enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_WO, K_W13, K_W2, K_LMHEAD, K_ATTN_WO, K_NCLASS };
 
 struct Profile {
     std::array<double, K_NCLASS> ms{};       // accumulated device time
@@ -51,6 +51,9 @@ struct Context {
     // bit-faithful VALU kernels (prompt_exact; env LVK_PROMPT_EXACT=1)
     bool prompt_exact = false;
     bool old_attention = false;
+    // single-token attention + Wo in one launch (k_attn_wo), env LVK_FUSE_ATTN_WO=1: bit-exact but
+    // measured slower than the two launches (17.7 vs 11.5 us per layer at n_past 256), so off
+    bool fuse_attn_wo = false;
     void * attn_gran = nullptr;  // [H][n_ctx] {tag, score} granules of the decode attention  // env LVK_ATTN_V1=1: single-token evals on the one-kernel attention.hip
     uint16_t * xh = nullptr;     // masked MFMA B-fragment image of the quantized activations (mm_act_bytes)
     float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales

@@ -105,7 +105,7 @@ _sig("lvk_stage_set_x", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_layers", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)])
 
 BLOCK_BYTES = {2: 20, 3: 24}
-KCLASS = ["embed", "qkv", "attention", "wo", "w13", "w2", "lm_head"]
+KCLASS = ["embed", "qkv", "attention", "wo", "w13", "w2", "lm_head", "attn_wo"]
 
 
 def _check(rc, what):

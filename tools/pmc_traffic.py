@@ -19,6 +19,8 @@ def klass(name):
     if m:
         pro, epi, kt = int(m.group(4)), int(m.group(5)), int(m.group(6))
         return {2: "qkv", 4: "w13", 0: "lm_head"}.get(epi) or ("wo" if kt == 4096 else "w2")
+    if "k_attn_wo" in name:
+        return "attn_wo"
     if "k_attn" in name:
         return "attention"
     return None
