@@ -462,11 +462,11 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         switch (cfg) { case 0: return go<a0, PR, E, K_>(P, s); case 1: return go<a1, PR, E, K_>(P, s); \
                        case 2: return go<a2, PR, E, K_>(P, s); default: return go<a3, PR, E, K_>(P, s); }
 #define C3(a, b, c) a, b, c
-        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(6, 0, 4), C3(12, 0, 2), C3(6, 2, 4))
-        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(8, 0, 4), C3(10, 0, 2), C3(8, 4, 2))
+        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(8, 0, 4), C3(6, 0, 4), C3(12, 0, 4))
+        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(12, 0, 4), C3(16, 0, 2), C3(16, 0, 4))
         if (K == 4096 && epi == EPI_STORE) SW4(EPI_STORE, PRO_NORM, 4096, C3(16, 0, 2), C3(8, 0, 4), C3(12, 0, 2), C3(8, 4, 2))
-        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 0, 4), C3(2, 2, 2), C3(4, 0, 2))
-        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(2, 2, 6), C3(2, 4, 4), C3(4, 0, 4), C3(2, 6, 6))
+        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 0, 4), C3(4, 0, 4), C3(4, 0, 2))
+        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(4, 0, 4), C3(4, 0, 11), C3(2, 0, 11), C3(4, 0, 8))
     }
 #endif
     if (K == 4096) {

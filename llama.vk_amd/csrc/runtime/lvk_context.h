@@ -6,6 +6,7 @@
 #include <array>
 #include <chrono>
 #include <functional>
+#include <new>
 
 struct llama_context_params;
 
@@ -13,6 +14,26 @@ namespace lvk {
 
 // kernel classes timed by the profiler (events around every launch of a class)
 enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_WO, K_W13, K_W2, K_LMHEAD, K_ATTN_WO, K_NCLASS };
+
+// page-locked host storage: the per-token logits D2H copy runs as one DMA instead of
+// being staged through a driver bounce buffer
+template <class T>
+struct PinnedAlloc {
+    using value_type = T;
+    PinnedAlloc() = default;
+    template <class U>
+    PinnedAlloc(const PinnedAlloc<U> &) {}
+    T * allocate(size_t n) {
+        void * p = nullptr;
+        if (hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+        return (T *) p;
+    }
+    void deallocate(T * p, size_t) { (void) hipHostFree(p); }
+    template <class U>
+    bool operator==(const PinnedAlloc<U> &) const { return true; }
+    template <class U>
+    bool operator!=(const PinnedAlloc<U> &) const { return false; }
+};
 
 struct Profile {
     std::array<double, K_NCLASS> ms{};       // accumulated device time
@@ -66,7 +87,7 @@ struct Context {
     bool use_graph = true;
 
     // host-visible results
-    std::vector<float> logits;
+    std::vector<float, PinnedAlloc<float>> logits;
     std::vector<float> embedding;
     std::vector<uint8_t> kv_host;
     int kv_n = 0;
