@@ -30,9 +30,11 @@
 //       xm[token tile][block][c][64 lanes] x 8 B
 //     (lane (h, jj, n): chain 2c+h of token n when h == jj, else zero), so a
 //     wave loads each fragment with one coalesced global_load_dwordx2 -- no
-//     LDS staging and no barrier per K step; 4 blocks are kept in flight.
+//     LDS staging and no barrier per K step; 2 blocks are kept in flight (a
+//     ring of 4 pushes the kernel past 256 VGPRs into scratch).
 //   Scales: dw (octet image) and da staged per 32-block chunk in LDS (one
-//     barrier per chunk).
+//     barrier per chunk); s = dw*da of 32 rows x 16 tokens x 2 blocks comes
+//     from one v_mfma_f32_32x32x1f32 outer product (exact f32 products).
 // Workgroup = 4 waves, tile 128 rows x 16 tokens (wave w: rows 32w..32w+31,
 // all 8 chains: 64 accumulator registers); workgroups are mapped so the 8
 // XCDs each sweep contiguous row tiles with the token tiles innermost (the
@@ -54,14 +56,14 @@ constexpr int TM = 128;     // rows per workgroup
 constexpr int TN = 16;      // tokens per workgroup (one token tile)
 constexpr int NT = 256;     // threads (4 waves)
 // LVK_MM_EXP (dev probe builds only, tools/probe), bit flags: 1 no fp32 chains, 2 no MFMA, 4 no B loads,
-// 8 no A loads, 16 no scale LDS reads
+// 8 no A loads
 #ifndef LVK_MM_EXP
 #define LVK_MM_EXP 0
 #endif
 #ifndef LVK_MM_PD
-#define LVK_MM_PD 4
+#define LVK_MM_PD 2
 #endif
-constexpr int PD = LVK_MM_PD;   // B blocks in flight per wave (ring size divides 8)
+constexpr int PD = LVK_MM_PD;   // B blocks in flight per wave (ring size divides 8; 4 spills at 256 VGPRs)
 
 constexpr int DWS = TM + 8;                         // padded row stride of the dw image (conflict-free stores)
 constexpr int DAS = TN + 1;                         // padded stride of the da image
