@@ -38,6 +38,7 @@
 #include "matvec_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace lvk {
@@ -45,6 +46,9 @@ namespace lvk {
 namespace {
 
 constexpr int HD = 128;
+#ifndef LVK_PROBE_WO_MODE   // dev probe builds only: 1 Wo workgroups idle, 2 Wo weights issued after the wait
+#define LVK_PROBE_WO_MODE 0
+#endif
 
 __device__ __forceinline__ void unpack8(const uint4 v, float f[8]) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -112,7 +116,9 @@ struct AttnDArgs {
     int exp_mode;
 };
 
-template <int QT>
+// EXCH: the 4 workgroups of a head split the scores and exchange them as granules;
+// !EXCH: every workgroup scores all positions itself (4x the K reads, from the XCD's L2)
+template <int QT, bool EXCH = true>
 __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, const int sl, uint8_t * smem) {
     const int E = A.E, n_ctx = A.n_ctx, d0 = h * HD + sl * 32;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = tid & 3;
@@ -135,7 +141,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     uint4 kv[2][4];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-        const int p = min(sl * 64 + c * 256 + (tid >> 2), n_ctx - 1);
+        const int p = min((EXCH ? sl * 64 + c * 256 : c * 64) + (tid >> 2), n_ctx - 1);
         const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
 #pragma unroll
         for (int st = 0; st < 4; ++st) kv[c][st] = kp[st * 4];
@@ -173,14 +179,17 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
             const float kq = quad_reduce(s);
             if (r == 0 && p < n_kv) {
                 const float v = kq * A.scale;                    // ggml_vec_scale_f32 (llama.cpp:1026)
-                __hip_atomic_store(g + p, ((unsigned long long) A.epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                if constexpr (!EXCH) sc[p] = v;
+                else __hip_atomic_store(g + p, ((unsigned long long) A.epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
         };
+        const int cs = EXCH ? 256 : 64;                     // position stride of this workgroup's chunks
+        const int cb = EXCH ? sl * 64 : 0;
 #pragma unroll
         for (int c = 0; c < 2; ++c)
-            if (sl * 64 + c * 256 < n_kv) score(kv[c], sl * 64 + c * 256 + (tid >> 2));
-        for (int c0 = sl * 64 + 512; c0 < n_kv; c0 += 256) {
+            if (cb + c * cs < n_kv) score(kv[c], cb + c * cs + (tid >> 2));
+        for (int c0 = cb + 2 * cs; c0 < n_kv; c0 += cs) {
             const int p = c0 + (tid >> 2);
             const uint4 * kp = (const uint4 *) (A.kc + (size_t) min(p, n_kv - 1) * E + h * HD) + r;
             uint4 k4[4];
@@ -192,8 +201,9 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     LVK_DT(2);
     // 2. every score of the head: poll each granule until it carries this layer's epoch
     float mx = -INFINITY;
+    if constexpr (!EXCH) __syncthreads();
     for (int p = tid; p < n_kv; p += 256) {
-        const float v = __uint_as_float((unsigned) poll_granule(g + p, A.epoch));
+        const float v = EXCH ? __uint_as_float((unsigned) poll_granule(g + p, A.epoch)) : sc[p];
         sc[p] = v;
         mx = v > mx ? v : mx;
     }
@@ -315,10 +325,10 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     }
 }
 
-template <int QT>
+template <int QT, bool EXCH>
 __global__ __launch_bounds__(256) void k_attn_d(AttnDArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    attn_d_run<QT>(A, blockIdx.x, blockIdx.y, smem);
+    attn_d_run<QT, EXCH>(A, blockIdx.x, blockIdx.y, smem);
 }
 
 // ---- k_attn_wo: the Wo workgroups (row length n_embd = 4096 compiled in) ----
@@ -348,7 +358,7 @@ __device__ __forceinline__ void wo_run(const WoArgs & P, unsigned long long * og
     const int g0 = (int) ((unsigned) b * (unsigned) P.G / (unsigned) P.nwg);
     const int g1 = (int) ((unsigned) (b + 1) * (unsigned) P.G / (unsigned) P.nwg);
     const int ng = (g1 - g0 - wave + NW - 1) / NW;       // row groups of this wave
-    if (ng <= 0) return;
+    if (ng <= 0 || LVK_PROBE_WO_MODE == 1) return;
     int gc = g0 + wave;
 
     // 1. the wave's first row group in flight before anything waits (matvec_cu.hip image
@@ -364,8 +374,16 @@ __device__ __forceinline__ void wo_run(const WoArgs & P, unsigned long long * og
         S[slot] = *(const float4 *) ((const char *) (P.scl + ((size_t) (grp) * NC + (cc)) * 64) + loff); \
         __builtin_amdgcn_sched_barrier(0);                                                               \
     } while (0)
+    if constexpr (LVK_PROBE_WO_MODE == 3) {
+        // let the attention's own loads go first: its start is bandwidth-bound, its
+        // score exchange and softmax are not
+        __builtin_amdgcn_s_sleep(127);
+        __builtin_amdgcn_s_sleep(127);
+    }
+    if constexpr (LVK_PROBE_WO_MODE != 2) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) LVK_WO_ISSUE(d, gc, d);
+        for (int d = 0; d < D; ++d) LVK_WO_ISSUE(d, gc, d);
+    }
 
     // 2. the Wo input: 5 granules per block from the attention workgroups, into this
     // wave's own activation table (matvec_common.h layout)
@@ -378,14 +396,20 @@ __device__ __forceinline__ void wo_run(const WoArgs & P, unsigned long long * og
     if (lane == 0) {
         // the attention takes several microseconds: sleep through most of it before the
         // first poll, then poll sparsely (hundreds of pollers on one word cost the chip)
-        __builtin_amdgcn_s_sleep(127);
-        __builtin_amdgcn_s_sleep(127);
+        if constexpr (LVK_PROBE_WO_MODE != 3) {
+            __builtin_amdgcn_s_sleep(127);
+            __builtin_amdgcn_s_sleep(127);
+        }
         for (int spins = 0; __hip_atomic_load((u32g *) ocount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
                             spins < (1 << 20);
              ++spins)
-            __builtin_amdgcn_s_sleep(16);
+            __builtin_amdgcn_s_sleep(LVK_PROBE_WO_MODE == 3 ? 4 : 16);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");     // no granule load above the wait
+    if constexpr (LVK_PROBE_WO_MODE == 2) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) LVK_WO_ISSUE(d, gc, d);
+    }
     u64g * og = (u64g *) ogran;
     static_assert(NB * 5 == 10 * 64, "granules per lane");
     unsigned long long gv[10];
@@ -518,10 +542,14 @@ hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned e
     if (A.out_qtype != Q4_0 && A.out_qtype != Q4_1) return hipErrorNotSupported;
     const AttnDArgs a = attn_args(A, gran, epoch);
     const size_t lds = attn_lds(A.n_ctx);
-    if (A.out_qtype == Q4_1)
-        LVK_LAUNCH(k_attn_d<Q4_1>, dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
-    else
-        LVK_LAUNCH(k_attn_d<Q4_0>, dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
+    static const bool exch = !(getenv("LVK_ATTN_NOEXCH") && atoi(getenv("LVK_ATTN_NOEXCH")) != 0);
+    if (A.out_qtype == Q4_1) {
+        if (exch) LVK_LAUNCH((k_attn_d<Q4_1, true>), dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
+        else LVK_LAUNCH((k_attn_d<Q4_1, false>), dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
+    } else {
+        if (exch) LVK_LAUNCH((k_attn_d<Q4_0, true>), dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
+        else LVK_LAUNCH((k_attn_d<Q4_0, false>), dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
+    }
     return hipGetLastError();
 }
 
