@@ -68,7 +68,8 @@ struct ActQ {
 struct StepParams {
     int n_past;
     int n_tokens;
-    int pad0, pad1;
+    int pad0;       // the token of a single-token eval (read by the embedding kernel)
+    int pad1;
 };
 
 struct RopeTable {            // host-built with glibc powf/cosf/sinf (ggml.c:7209-7213)

@@ -261,7 +261,10 @@ void Context::enqueue_forward(int n, bool last_only) {
         // the decode attention's score granules carry epoch = layer + 1: zero them once per token
         LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes(H, n_ctx), stream));
     if (model.has_embed)
-        timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_d, n, x, stream); });
+        // a single-token eval takes its token from the step block (one H2D copy per token)
+        timed_launch(K_EMBED, 0, [&] {
+            return launch_embed(model.tok_emb, model.emb_type, E, n == 1 ? &sp_d->pad0 : tok_d, n, x, stream);
+        });
     for (size_t il = 0; il < model.layers.size(); ++il) {
         const Layer & ly = model.layers[il];
         MvLaunch a;
@@ -312,9 +315,15 @@ void Context::enqueue_forward(int n, bool last_only) {
 }
 
 void Context::build_graph() {
+    // one replay per token: the step block H2D, the forward pass and the logits D2H
+    // (both host buffers page-locked, the logits one sized before the capture)
     LVK_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
+        LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
         enqueue_forward(1, true);
+        if (model.has_head)
+            LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost,
+                                   stream));
     } catch (...) {
         hipGraph_t g;
         (void) hipStreamEndCapture(stream, &g);
@@ -336,19 +345,20 @@ void Context::eval(const int * tokens, int n, int n_past) {
     }
     sp_h->n_past = n_past;
     sp_h->n_tokens = n;
-    LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
-    LVK_HIP(hipMemcpyAsync(tok_d, tok_h, sizeof(int) * (size_t) n, hipMemcpyHostToDevice, stream));
+    sp_h->pad0 = (n == 1 && model.has_embed) ? tokens[0] : 0;
     const bool last_only = !logits_all;
+    const int rows = last_only ? 1 : n;
+    if (model.has_head) logits.resize((size_t) rows * V);   // within the reserve: the pointer never moves
     if (n == 1 && last_only && use_graph && !profiling) {
         if (!graph_exec) build_graph();
         LVK_HIP(hipGraphLaunch(graph_exec, stream));
     } else {
+        LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
+        if (n > 1) LVK_HIP(hipMemcpyAsync(tok_d, tok_h, sizeof(int) * (size_t) n, hipMemcpyHostToDevice, stream));
         enqueue_forward(n, last_only);
-    }
-    const int rows = last_only ? 1 : n;
-    if (model.has_head) {
-        logits.resize((size_t) rows * V);
-        LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost, stream));
+        if (model.has_head)
+            LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost,
+                                   stream));
     }
     if (want_embedding && model.has_head) {
         embedding.resize(hp.n_embd);
