@@ -226,6 +226,22 @@ def main():
     elapsed = all_max(pg, t1 - t0)
     value = n_gpus * args.steps / elapsed
 
+    # same decode with the sampler on the device (lvk_eval_greedy): the
+    # argmax runs over the logits in HBM and 4 bytes come back instead of 128 KB
+    m.eval(ptoks, 0)
+    tok = int(np.argmax(m.logits()[-1]))
+    tok_first = tok
+    barrier(pg)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        tok = m.eval_greedy(tok, 16 + (i % (n_ctx - 16)))
+    t1 = time.perf_counter()
+    barrier(pg)
+    el_g = all_max(pg, t1 - t0)
+    greedy = {"value": n_gpus * args.steps / el_g, "unit": "tok/s", "ms_per_step": el_g / args.steps * 1e3,
+              "path": "lvk_eval_greedy: decode graph ending in the device argmax, 4-byte D2H",
+              "first_token": tok_first}
+
     # prompt eval: one 512-token batch (configs[2])
     p512 = np.array(prompt_tokens(512), np.int32)
     best = 1e30
@@ -338,6 +354,7 @@ def main():
             "step_roofline": {"model_bytes_per_token": MODEL_BYTES_7B, "achieved_gbs": step_gbs,
                               "frac": step_gbs / HBM_PEAK_GBS, "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_7B},
             "prompt_eval": prompt,
+            "decode_greedy_device": greedy,
             "decode_13b_q4_1": q41,
             "layer_split": split,
             "kernels": kernels,

@@ -103,6 +103,17 @@ LVK_API void lvk_set_prompt_exact(struct llama_context * ctx, int on);
 /* 1 = replay the captured decode graph for single-token evals (default), 0 = eager */
 LVK_API void lvk_set_graph(struct llama_context * ctx, int on);
 
+/* On-device greedy sampling.  lvk_eval_greedy(ctx, token, n_past)
+ * is llama_eval(ctx, &token, 1, n_past, .) followed by
+ * llama_sample_top_p_top_k(ctx, ., ., ., ., temp <= 0) (llama.cpp:1703-1719,
+ * 1382-1394): the argmax runs over the logits in HBM and only the 4-byte token
+ * crosses PCIe.  Returns the next token id, or -1 on error (message on stderr).
+ * The host logits of llama_get_logits are NOT refreshed by this call.
+ * lvk_argmax(x, n) is the op-level kernel on a host array: the first index whose
+ * value is strictly greater than all earlier ones (0 when x[0] is NaN). */
+LVK_API int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past);
+LVK_API int lvk_argmax(const float * x, int n);
+
 /* Pipeline stages (the 65B layer split).  A stage context holds
  * layers [layer_begin, layer_end) of the model file (weights and KV cache); the
  * first stage (layer_begin == 0) also holds the token embeddings, the last one

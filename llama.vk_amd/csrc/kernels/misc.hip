@@ -3,6 +3,7 @@
 #include "lvk_device.h"
 #include "lvk_kernels.h"
 #include "matvec_common.h"
+#include <climits>
 
 namespace lvk {
 thread_local LaunchEvents g_launch_events;
@@ -235,6 +236,54 @@ __global__ __launch_bounds__(256) void k_rmsnorm_rows(const float * __restrict__
 
 hipError_t launch_rmsnorm_rows(const float * x, const float * g, int K, int n, float * y, hipStream_t s) {
     hipLaunchKernelGGL(k_rmsnorm_rows, dim3(n), dim3(256), 0, s, x, g, K, y);
+    return hipGetLastError();
+}
+}  // namespace lvk
+
+namespace lvk {
+namespace {
+// Greedy token choice on the device (llama.cpp:1382-1394): the first index whose
+// logit is strictly greater than every earlier one.  Sequentially that is
+// "index 0 if x[0] is NaN, else the first maximum over the non-NaN entries"
+// (NaN never compares greater, and nothing beats a NaN start).  One workgroup:
+// each thread scans a strided slice in increasing index order, then the
+// (value, index) pairs reduce with ties going to the lower index.
+struct ArgBest {
+    float v;
+    int i;   // INT_MAX: no non-NaN entry seen
+};
+__device__ inline ArgBest arg_pick(ArgBest a, ArgBest b) {
+    if (b.i == INT_MAX) return a;
+    if (a.i == INT_MAX) return b;
+    return (b.v > a.v || (b.v == a.v && b.i < a.i)) ? b : a;
+}
+__global__ __launch_bounds__(1024) void k_argmax_first(const float * __restrict__ x, int n, int * __restrict__ out) {
+    __shared__ ArgBest red[16];
+    ArgBest b{-INFINITY, INT_MAX};
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const float v = x[i];
+        if (v == v && (b.i == INT_MAX || v > b.v)) b = {v, i};
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        ArgBest o;
+        o.v = __shfl_xor(b.v, off, 64);
+        o.i = __shfl_xor(b.i, off, 64);
+        b = arg_pick(b, o);
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ArgBest r = red[0];
+        for (int w = 1; w < 16; ++w) r = arg_pick(r, red[w]);
+        const bool nan0 = n > 0 && !(x[0] == x[0]);
+        out[0] = (nan0 || r.i == INT_MAX) ? 0 : r.i;
+    }
+}
+}  // namespace
+
+hipError_t launch_argmax(const float * x, int n, int * out, hipStream_t s) {
+    if (n <= 0) return hipErrorInvalidValue;
+    LVK_LAUNCH(k_argmax_first, dim3(1), dim3(1024), 0, s, x, n, out);
     return hipGetLastError();
 }
 }  // namespace lvk

@@ -62,6 +62,9 @@ int pick_exp_mode(const uint16_t * exp_tab_d) {
 Context::~Context() {
     if (graph_exec) (void) hipGraphExecDestroy(graph_exec);
     if (graph) (void) hipGraphDestroy(graph);
+    if (graph_greedy_exec) (void) hipGraphExecDestroy(graph_greedy_exec);
+    if (graph_greedy) (void) hipGraphDestroy(graph_greedy);
+    if (greedy_h) (void) hipHostFree(greedy_h);
     for (auto & e : ev_pool) { (void) hipEventDestroy(e.first); (void) hipEventDestroy(e.second); }
     if (sp_h) (void) hipHostFree(sp_h);
     if (tok_h) (void) hipHostFree(tok_h);
@@ -110,6 +113,8 @@ void Context::init(const llama_context_params & p) {
     tok_d = (int *) model.alloc(C * 4);
     LVK_HIP(hipHostMalloc((void **) &sp_h, sizeof(StepParams), hipHostMallocDefault));
     LVK_HIP(hipHostMalloc((void **) &tok_h, C * 4, hipHostMallocDefault));
+    greedy_d = (int *) model.alloc(4);
+    LVK_HIP(hipHostMalloc((void **) &greedy_h, 4, hipHostMallocDefault));
 
     // fp16 exp / silu tables (ggml.c:2915-2927), built with this host's glibc
     std::vector<uint16_t> te, ts;
@@ -314,23 +319,57 @@ void Context::enqueue_forward(int n, bool last_only) {
         LVK_HIP(launch_rmsnorm_rows(x + (size_t) (n - 1) * E, model.norm, E, 1, emb_d, stream));
 }
 
-void Context::build_graph() {
+void Context::build_graph(bool greedy) {
     // one replay per token: the step block H2D, the forward pass and the logits D2H
-    // (both host buffers page-locked, the logits one sized before the capture)
+    // (both host buffers page-locked, the logits one sized before the capture); the
+    // greedy variant ends in the device argmax and copies back 4 bytes instead
     LVK_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
         LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
         enqueue_forward(1, true);
-        if (model.has_head)
+        if (greedy) {
+            LVK_HIP(launch_argmax(logits_d, (int) model.hp.n_vocab, greedy_d, stream));
+            LVK_HIP(hipMemcpyAsync(greedy_h, greedy_d, sizeof(int), hipMemcpyDeviceToHost, stream));
+        } else if (model.has_head) {
             LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost,
                                    stream));
+        }
     } catch (...) {
         hipGraph_t g;
         (void) hipStreamEndCapture(stream, &g);
         throw;
     }
-    LVK_HIP(hipStreamEndCapture(stream, &graph));
-    LVK_HIP(hipGraphInstantiate(&graph_exec, graph, nullptr, nullptr, 0));
+    hipGraph_t & g = greedy ? graph_greedy : graph;
+    hipGraphExec_t & ge = greedy ? graph_greedy_exec : graph_exec;
+    LVK_HIP(hipStreamEndCapture(stream, &g));
+    LVK_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+}
+
+// One decode step whose sampler is greedy, chosen on the device:
+// the same forward pass and KV append as eval(&token, 1, n_past), then the argmax
+// of llama_sample_top_p_top_k(temp <= 0) (llama.cpp:1382-1394) over the logits in
+// HBM.  Host logits are not refreshed (llama_get_logits keeps the previous eval's).
+int Context::eval_greedy(int token, int n_past) {
+    const int V = (int) model.hp.n_vocab;
+    if (!model.has_head || !model.has_embed) throw Error("llama.vk_amd: greedy eval needs the whole model");
+    if (n_past < 0 || n_past + 1 > n_ctx) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
+    if (token < 0 || token >= V) throw Error("llama.vk_amd: token id out of range");
+    tok_h[0] = token;
+    sp_h->n_past = n_past;
+    sp_h->n_tokens = 1;
+    sp_h->pad0 = token;
+    if (use_graph && !profiling) {
+        if (!graph_greedy_exec) build_graph(true);
+        LVK_HIP(hipGraphLaunch(graph_greedy_exec, stream));
+    } else {
+        LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
+        enqueue_forward(1, true);
+        LVK_HIP(launch_argmax(logits_d, V, greedy_d, stream));
+        LVK_HIP(hipMemcpyAsync(greedy_h, greedy_d, sizeof(int), hipMemcpyDeviceToHost, stream));
+    }
+    LVK_HIP(hipStreamSynchronize(stream));
+    if (profiling) collect_profile();
+    return *greedy_h;
 }
 
 void Context::eval(const int * tokens, int n, int n_past) {

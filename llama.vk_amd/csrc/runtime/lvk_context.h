@@ -85,6 +85,11 @@ struct Context {
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     bool use_graph = true;
+    // greedy decode graph (lvk_eval_greedy): argmax on the device, 4-byte D2H instead of the logits row
+    hipGraph_t graph_greedy = nullptr;
+    hipGraphExec_t graph_greedy_exec = nullptr;
+    int * greedy_d = nullptr;
+    int * greedy_h = nullptr;    // pinned
 
     // host-visible results
     std::vector<float, PinnedAlloc<float>> logits;
@@ -112,7 +117,8 @@ struct Context {
     void x_copy(void * buf, int n, bool to_ctx, bool on_device);
     void enqueue_forward(int n, bool last_only);
     bool use_mfma(int n) const;
-    void build_graph();
+    void build_graph(bool greedy = false);
+    int eval_greedy(int token, int n_past);
     void kv_get();
     void kv_set(const uint8_t * src, size_t n);
     size_t kv_bytes() const;

@@ -286,4 +286,32 @@ void lvk_set_graph(struct llama_context * ctx, int on) { ctx->c.use_graph = on !
 
 void lvk_set_prompt_exact(struct llama_context * ctx, int on) { ctx->c.prompt_exact = on != 0; }
 
+int lvk_argmax(const float * x, int n) {
+    try {
+        if (n <= 0) throw lvk::Error("n must be positive");
+        Dev dv;
+        float * xd = dv.up(x, (size_t) n);
+        int * od = (int *) dv.get(4);
+        int r = -1;
+        LVK_HIP(lvk::launch_argmax(xd, n, od, nullptr));
+        LVK_HIP(hipMemcpy(&r, od, 4, hipMemcpyDeviceToHost));
+        return r;
+    } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
+int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past) {
+    lvk::Context & c = ctx->c;
+    const int64_t t0 = lvk::now_us();
+    int r;
+    try {
+        r = c.eval_greedy(token, n_past);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: failed to eval: %s\n", __func__, e.msg.c_str());
+        return -1;
+    }
+    c.t_eval_us += lvk::now_us() - t0;   // counted as a decode eval (llama.cpp:1186-1195)
+    c.n_eval++;
+    return r;
+}
+
 }  // extern "C"

@@ -98,6 +98,8 @@ _sig("lvk_reset_profile", None, [C.c_void_p])
 _sig("lvk_weight_bytes", C.c_size_t, [C.c_void_p])
 _sig("lvk_set_graph", None, [C.c_void_p, C.c_int])
 _sig("lvk_set_prompt_exact", None, [C.c_void_p, C.c_int])
+_sig("lvk_eval_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int])
+_sig("lvk_argmax", C.c_int, [f32p, C.c_int])
 _sig("lvk_init_stage", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, C.c_int])
 _sig("lvk_stage_eval", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_get_x", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
@@ -145,6 +147,14 @@ class Llama:
         _check(lib.llama_eval(self.ctx, t, len(t), n_past, n_threads), "llama_eval")
         self._last_n = len(t)
         return self.logits()
+
+    def eval_greedy(self, token, n_past):
+        """decode one token and pick the next greedily on the device (lvk_eval_greedy);
+        host logits are not refreshed"""
+        r = lib.lvk_eval_greedy(self.ctx, int(token), int(n_past))
+        if r < 0:
+            raise RuntimeError("lvk_eval_greedy failed")
+        return r
 
     # ---- pipeline stage (lvk_init_stage contexts)
     def stage_eval(self, tokens, n_tokens, n_past):
@@ -321,6 +331,15 @@ def attention_scores(kc, vc, q, n_embd, n_head, n_ctx, n_past, n):
 def exp_table_mismatches():
     """Arguments h <= 0 where the device's computed exp differs from table_exp_f16."""
     return int(lib.lvk_exp_table_mismatches())
+
+
+def argmax(x):
+    """device greedy argmax (first strict maximum; 0 when x[0] is NaN)"""
+    x = np.ascontiguousarray(x, np.float32).ravel()
+    r = lib.lvk_argmax(x, x.size)
+    if r < 0:
+        raise RuntimeError("lvk_argmax failed")
+    return r
 
 
 def rms_norm_mul(x, g):

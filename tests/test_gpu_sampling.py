@@ -1,0 +1,116 @@
+"""On-device greedy sampling against the reference's greedy rule.
+
+The reference picks, for temp <= 0, the first index whose logit is strictly
+greater than every earlier one (llama.cpp:1382-1394).  `ref_greedy` restates
+that loop; the device argmax (lvk_argmax) and the greedy decode step
+(lvk_eval_greedy) must choose the same token on the same logits, including
+ties, -inf rows and NaN entries.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def ref_greedy(row):
+    """llama.cpp:1382-1394, element by element"""
+    best, idx = row[0], 0
+    for i in range(1, len(row)):
+        if row[i] > best:
+            best, idx = row[i], i
+    return idx
+
+
+@pytest.fixture(scope="module")
+def lvk(gpu_available):
+    import lvk as m
+    return m
+
+
+def _cases():
+    rng = np.random.default_rng(5)
+    yield "random_32000", rng.standard_normal(32000).astype(np.float32)
+    x = rng.standard_normal(32000).astype(np.float32)
+    x[[17, 9000, 31999]] = 9.0
+    yield "ties_first_wins", x
+    yield "all_equal", np.full(4097, 2.5, np.float32)
+    yield "all_neg_inf", np.full(1000, -np.inf, np.float32)
+    x = np.full(3000, -np.inf, np.float32)
+    x[2999] = -1e30
+    yield "max_at_last", x
+    x = rng.standard_normal(5000).astype(np.float32)
+    x[0] = np.nan
+    yield "nan_at_0", x
+    x = rng.standard_normal(5000).astype(np.float32)
+    x[[3, 70, 4999]] = np.nan
+    x[1234] = 50.0
+    yield "nan_inside", x
+    yield "single", np.array([-3.0], np.float32)
+    yield "n_1025", rng.standard_normal(1025).astype(np.float32)
+    x = np.zeros(2048, np.float32)
+    x[1] = -0.0
+    x[5] = np.float32(1e-45)
+    yield "signed_zero_denormal", x
+
+
+@pytest.mark.parametrize("name,x", list(_cases()), ids=[c[0] for c in _cases()])
+def test_device_argmax_matches_reference_rule(lvk, name, x):
+    assert lvk.argmax(x) == ref_greedy(x.tolist())
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_greedy_decode_matches_host_greedy(lvk, tiny_models, graph):
+    """eval_greedy's token stream equals llama_eval + the reference's greedy over host logits"""
+    path = tiny_models["tiny_q4_0"]
+    a = lvk.Llama(path, n_ctx=256)
+    b = lvk.Llama(path, n_ctx=256)
+    a.set_graph(graph)
+    b.set_graph(graph)
+    toks = np.array([1, 450, 4996, 17354, 1701, 29916], np.int32)
+    la = a.eval(toks, 0)
+    b.eval(toks, 0)
+    n_past, tok = len(toks), ref_greedy(la[-1].tolist())
+    for _ in range(40):
+        la = a.eval([tok], n_past)
+        want = ref_greedy(la[-1].tolist())
+        got = b.eval_greedy(tok, n_past)
+        assert got == want, "n_past %d" % n_past
+        n_past += 1
+        tok = want
+    # both contexts hold the same KV cache afterwards
+    assert np.array_equal(a.kv_cache(), b.kv_cache())
+    a.close()
+    b.close()
+
+
+def test_greedy_decode_7b_shaped_vs_oracle(lvk, oracle, model_dir):
+    """LLaMA-7B layer shapes (2 layers): the device greedy tokens follow the oracle's logits"""
+    from oracle_lib import gen_model
+    path = gen_model(os.path.join(model_dir, "w4096_l2.bin"), n_embd=4096, n_head=32, n_layer=2, ftype=2, seed=7)
+    m = lvk.Llama(path, n_ctx=512)
+    m.set_prompt_exact(True)
+    om = oracle.model(path, 512)
+    toks = np.array([1, 450, 4996, 17354, 1701, 29916, 338, 263], np.int32)
+    m.eval(toks, 0)
+    b = om.eval(toks, 0)
+    n_past, tok = len(toks), ref_greedy(b[-1].tolist())
+    for _ in range(10):
+        got = m.eval_greedy(tok, n_past)
+        b = om.eval([tok], n_past)
+        assert got == ref_greedy(b[-1].tolist()), "n_past %d" % n_past
+        n_past += 1
+        tok = got
+    m.close()
+    om.close()
+
+
+def test_greedy_decode_errors(lvk, tiny_models):
+    m = lvk.Llama(tiny_models["tiny_q4_0"], n_ctx=64)
+    with pytest.raises(RuntimeError):
+        m.eval_greedy(10 ** 6, 0)          # token id out of range
+    with pytest.raises(RuntimeError):
+        m.eval_greedy(1, 64)               # n_past + 1 > n_ctx
+    assert m.eval_greedy(1, 0) >= 0        # the context still works
+    m.close()
