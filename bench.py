@@ -241,6 +241,13 @@ def main():
     greedy = {"value": n_gpus * args.steps / el_g, "unit": "tok/s", "ms_per_step": el_g / args.steps * 1e3,
               "path": "lvk_eval_greedy: decode graph ending in the device argmax, 4-byte D2H",
               "first_token": tok_first}
+    # host sampler (llama_sample_top_p_top_k, main's defaults: top_k 40, top_p 0.95, temp 0.8,
+    # repeat_penalty 1.1 over a 64-token window) on the last logits
+    last64 = np.array(prompt_tokens(64), np.int32)
+    t0 = time.perf_counter()
+    for _ in range(200):
+        m.sample(last64, 40, 0.95, 0.8, 1.1)
+    greedy["host_sampler_us"] = (time.perf_counter() - t0) / 200 * 1e6
 
     # prompt eval: one 512-token batch (configs[2])
     p512 = np.array(prompt_tokens(512), np.int32)

@@ -105,8 +105,13 @@ int sample_top_p_top_k(lvk::Context & c, const std::vector<int> & last, int top_
     std::vector<std::pair<float, int>> cand;
     cand.reserve(n_logits);
     const float scale = 1.0f / temp;
+    // membership in last_n as a flag per id: the reference's std::find per logit
+    // (llama.cpp:1404) costs n_vocab * last_n compares (~2M at 32000 x 64)
+    std::vector<uint8_t> in_last((size_t) n_logits, 0);
+    for (const int t : last)
+        if (t >= 0 && t < n_logits) in_last[(size_t) t] = 1;
     for (int i = 0; i < n_logits; ++i) {
-        if (std::find(last.begin(), last.end(), i) != last.end()) {
+        if (in_last[(size_t) i]) {
             if (pl[i] < 0.0f) cand.emplace_back(pl[i] * scale * repeat_penalty, i);
             else cand.emplace_back(pl[i] * scale / repeat_penalty, i);
         } else {

@@ -126,6 +126,7 @@ class Ref:
         _sig(L, "ref_eval", C.c_int, [C.c_void_p, i32p, C.c_int, C.c_int, C.c_int])
         _sig(L, "ref_get_logits", None, [C.c_void_p, f32p, C.c_int])
         _sig(L, "ref_n_vocab", C.c_int, [C.c_void_p])
+        _sig(L, "ref_sample", C.c_int, [C.c_void_p, i32p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float])
         _sig(L, "ref_tokenize", C.c_int, [C.c_void_p, C.c_char_p, i32p, C.c_int, C.c_int])
         _sig(L, "ref_quantize_row", None, [C.c_int, f32p, u8p, C.c_int])
         _sig(L, "ref_quantize_row_reference", None, [C.c_int, f32p, u8p, C.c_int])
@@ -172,6 +173,11 @@ class RefModel:
         out = np.zeros(rows * self.n_vocab, np.float32)
         self.ref.lib.ref_get_logits(self.h, out, out.size)
         return out.reshape(rows, self.n_vocab)
+
+    def sample(self, last_tokens, top_k, top_p, temp, repeat_penalty):
+        """llama_sample_top_p_top_k of the reference build (llama.cpp:1777-1805)"""
+        t = np.ascontiguousarray(last_tokens, np.int32)
+        return self.ref.lib.ref_sample(self.h, t, len(t), top_k, top_p, temp, repeat_penalty)
 
     def close(self):
         if self.h:

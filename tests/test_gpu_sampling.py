@@ -114,3 +114,31 @@ def test_greedy_decode_errors(lvk, tiny_models):
         m.eval_greedy(1, 64)               # n_past + 1 > n_ctx
     assert m.eval_greedy(1, 0) >= 0        # the context still works
     m.close()
+
+
+@pytest.mark.parametrize("top_k,top_p,temp,rp", [(40, 0.95, 0.8, 1.1), (0, 1.0, 1.0, 1.0), (5, 0.5, 0.3, 1.3),
+                                                 (1, 0.9, 2.0, 1.1), (40, 0.95, 0.0, 1.1)])
+def test_host_sampler_matches_reference_build(lvk, ref, tiny_models, top_k, top_p, temp, rp):
+    """llama_sample_top_p_top_k against the reference build (oracle/_ref/libref.so) over a
+    40-step sampled decode: same seed (1), same last_n window (main.cpp's 64 zeros then the
+    tokens), bit-identical logits -> the same token stream"""
+    path = tiny_models["tiny_q4_0"]
+    m = lvk.Llama(path, n_ctx=256, seed=1)
+    m.set_prompt_exact(True)
+    r = ref.model(path, 256)
+    toks = np.array([1, 450, 4996, 17354, 1701, 29916], np.int32)
+    last = [0] * (64 - len(toks)) + toks.tolist()
+    a = m.eval(toks, 0)
+    b = r.eval(toks, 0)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    n_past = len(toks)
+    for step in range(40):
+        want = r.sample(last, top_k, top_p, temp, rp)
+        got = m.sample(last, top_k=top_k, top_p=top_p, temp=temp, repeat_penalty=rp)
+        assert got == want, "step %d" % step
+        last = last[1:] + [got]
+        m.eval([got], n_past)
+        r.eval([got], n_past)
+        n_past += 1
+    m.close()
+    r.close()
