@@ -66,3 +66,39 @@ def test_dropin_main_greedy_text_matches_reference_cpu(tiny_models):
     assert gpu_out == cpu_out
     assert len(gpu_out) > 60
     assert b"llama_print_timings" in gpu_err
+
+
+def _ppl_values(out):
+    """the `[i]ppl,` fields examples/perplexity prints (perplexity.cpp:76)"""
+    import re
+    return [(int(a), float(b)) for a, b in re.findall(rb"\[(\d+)\]([0-9.]+),", out)]
+
+
+@pytest.mark.gpu
+def test_dropin_perplexity_matches_reference_cpu(tiny_models, tmp_path):
+    """examples/perplexity (logits_all, n_ctx-token batches) on the GPU library vs the
+    reference build: the same running perplexity after every chunk."""
+    exe = os.path.join(DROPIN, "perplexity")
+    ref_exe = os.path.join(ROOT, "oracle", "_ref", "perplexity")
+    _need(exe)
+    _need(ref_exe)
+    words = ["the", "model", "reads", "every", "token", "of", "this", "text", "and", "predicts", "next",
+             "one", "from", "its", "context", "window", "while", "perplexity", "measures", "surprise"]
+    text = " ".join(words[(i * 7) % len(words)] + ("." if i % 11 == 10 else "") for i in range(600))
+    f = tmp_path / "ppl.txt"
+    f.write_text(text)
+    args = ["-m", tiny_models["tiny_q4_0"], "-f", str(f), "-c", "128", "-s", "1"]
+    cpu_out, _ = _run([ref_exe] + args + ["-t", "8"])
+    want = _ppl_values(cpu_out)
+    assert len(want) >= 3
+    os.environ["LVK_PROMPT_EXACT"] = "1"
+    try:
+        exact_out, _ = _run([exe] + args + ["-t", "1"])
+    finally:
+        del os.environ["LVK_PROMPT_EXACT"]
+    assert _ppl_values(exact_out) == want        # bit-exact logits -> the same printed digits
+    mfma_out, _ = _run([exe] + args + ["-t", "1"])
+    got = _ppl_values(mfma_out)
+    assert [i for i, _ in got] == [i for i, _ in want]
+    for (_, a), (_, b) in zip(got, want):
+        assert abs(a - b) <= 1e-3 * b
