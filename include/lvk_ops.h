@@ -114,6 +114,13 @@ LVK_API void lvk_set_graph(struct llama_context * ctx, int on);
 LVK_API int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past);
 LVK_API int lvk_argmax(const float * x, int n);
 
+/* Device-side KV state (the host-bytes form is llama_get_kv_cache /
+ * llama_set_kv_cache, llama.cpp:1678-1701): copy positions [0, n_tokens) of every
+ * layer's K and V from src to dst in HBM (same model shape and n_ctx, same device) and
+ * set dst's KV token count to n_tokens.  dst can then continue with
+ * llama_eval(dst, ., ., n_past = n_tokens, .) exactly as src would.  0 / -1. */
+LVK_API int lvk_kv_copy(struct llama_context * dst, struct llama_context * src, int n_tokens);
+
 /* Pipeline stages (the 65B layer split).  A stage context holds
  * layers [layer_begin, layer_end) of the model file (weights and KV cache); the
  * first stage (layer_begin == 0) also holds the token embeddings, the last one

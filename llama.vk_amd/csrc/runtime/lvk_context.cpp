@@ -425,6 +425,25 @@ void Context::kv_set(const uint8_t * src, size_t n) {
     LVK_HIP(hipMemcpy(vc, src + half, half, hipMemcpyHostToDevice));
 }
 
+// device-to-device copy of positions [0, n_tokens) of every layer's K and V from
+// another context of the same shape (a shared prompt prefix): K rows
+// [L][n_ctx][E] are one pitched block per layer, V [L][E][n_ctx] one short row per
+// (layer, dim).  Only the n_tokens positions move, not the whole cache.
+void Context::kv_copy_from(const Context & src, int n_tokens) {
+    const size_t E = model.hp.n_embd, L = model.layers.size(), C = (size_t) n_ctx;
+    if (src.model.hp.n_embd != model.hp.n_embd || src.model.layers.size() != L || src.n_ctx != n_ctx)
+        throw Error("lvk_kv_copy: contexts differ in n_embd, n_layer or n_ctx");
+    if (n_tokens < 0 || n_tokens > n_ctx) throw Error("lvk_kv_copy: n_tokens out of range");
+    if (n_tokens > 0) {
+        const size_t n = (size_t) n_tokens;
+        LVK_HIP(hipStreamSynchronize(src.stream));
+        LVK_HIP(hipMemcpy2DAsync(kc, C * E * 2, src.kc, C * E * 2, n * E * 2, L, hipMemcpyDeviceToDevice, stream));
+        LVK_HIP(hipMemcpy2DAsync(vc, C * 2, src.vc, C * 2, n * 2, L * E, hipMemcpyDeviceToDevice, stream));
+        LVK_HIP(hipStreamSynchronize(stream));
+    }
+    kv_n = n_tokens;
+}
+
 }  // namespace lvk
 
 namespace lvk {

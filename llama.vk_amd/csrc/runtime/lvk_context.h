@@ -121,6 +121,7 @@ struct Context {
     int eval_greedy(int token, int n_past);
     void kv_get();
     void kv_set(const uint8_t * src, size_t n);
+    void kv_copy_from(const Context & src, int n_tokens);
     size_t kv_bytes() const;
     void timed_launch(int cls, double bytes, const std::function<hipError_t()> & fn);
     void collect_profile();

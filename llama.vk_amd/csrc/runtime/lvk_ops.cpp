@@ -286,6 +286,14 @@ void lvk_set_graph(struct llama_context * ctx, int on) { ctx->c.use_graph = on !
 
 void lvk_set_prompt_exact(struct llama_context * ctx, int on) { ctx->c.prompt_exact = on != 0; }
 
+int lvk_kv_copy(struct llama_context * dst, struct llama_context * src, int n_tokens) {
+    try {
+        if (!dst || !src || dst == src) throw lvk::Error("need two distinct contexts");
+        dst->c.kv_copy_from(src->c, n_tokens);
+        return 0;
+    } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
 int lvk_argmax(const float * x, int n) {
     try {
         if (n <= 0) throw lvk::Error("n must be positive");

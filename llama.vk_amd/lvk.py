@@ -100,6 +100,7 @@ _sig("lvk_set_graph", None, [C.c_void_p, C.c_int])
 _sig("lvk_set_prompt_exact", None, [C.c_void_p, C.c_int])
 _sig("lvk_eval_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_argmax", C.c_int, [f32p, C.c_int])
+_sig("lvk_kv_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_int])
 _sig("lvk_init_stage", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, C.c_int])
 _sig("lvk_stage_eval", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_get_x", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
@@ -147,6 +148,13 @@ class Llama:
         _check(lib.llama_eval(self.ctx, t, len(t), n_past, n_threads), "llama_eval")
         self._last_n = len(t)
         return self.logits()
+
+    def kv_cache_token_count(self):
+        return lib.llama_get_kv_cache_token_count(self.ctx)
+
+    def kv_copy_from(self, src, n_tokens):
+        """take positions [0, n_tokens) of src's KV cache, device to device (lvk_kv_copy)"""
+        _check(lib.lvk_kv_copy(self.ctx, src.ctx, int(n_tokens)), "lvk_kv_copy")
 
     def eval_greedy(self, token, n_past):
         """decode one token and pick the next greedily on the device (lvk_eval_greedy);
