@@ -178,6 +178,8 @@ def main():
     ap.add_argument("--prompt-evals", type=int, default=3)
     ap.add_argument("--profile-steps", type=int, default=48)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-greedy", action="store_true",
+                    help="skip the lvk_eval_greedy decode leg (rocprofv3 kernel-trace runs, DESIGN.md section 9)")
     ap.add_argument("--no-13b", action="store_true", help="skip the 13B Q4_1 decode line (BASELINE configs[3])")
     ap.add_argument("--steps-13b", type=int, default=96)
     ap.add_argument("--no-split", action="store_true", help="N>1: skip the layer-split pipeline line (SURVEY 8e)")
@@ -226,28 +228,30 @@ def main():
     elapsed = all_max(pg, t1 - t0)
     value = n_gpus * args.steps / elapsed
 
-    # same decode with the sampler on the device (lvk_eval_greedy): the
-    # argmax runs over the logits in HBM and 4 bytes come back instead of 128 KB
-    m.eval(ptoks, 0)
-    tok = int(np.argmax(m.logits()[-1]))
-    tok_first = tok
-    barrier(pg)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        tok = m.eval_greedy(tok, 16 + (i % (n_ctx - 16)))
-    t1 = time.perf_counter()
-    barrier(pg)
-    el_g = all_max(pg, t1 - t0)
-    greedy = {"value": n_gpus * args.steps / el_g, "unit": "tok/s", "ms_per_step": el_g / args.steps * 1e3,
-              "path": "lvk_eval_greedy: decode graph ending in the device argmax, 4-byte D2H",
-              "first_token": tok_first}
-    # host sampler (llama_sample_top_p_top_k, main's defaults: top_k 40, top_p 0.95, temp 0.8,
-    # repeat_penalty 1.1 over a 64-token window) on the last logits
-    last64 = np.array(prompt_tokens(64), np.int32)
-    t0 = time.perf_counter()
-    for _ in range(200):
-        m.sample(last64, 40, 0.95, 0.8, 1.1)
-    greedy["host_sampler_us"] = (time.perf_counter() - t0) / 200 * 1e6
+    greedy = None
+    if not args.no_greedy:
+        # same decode with the sampler on the device (lvk_eval_greedy): the
+        # argmax runs over the logits in HBM and 4 bytes come back instead of 128 KB
+        m.eval(ptoks, 0)
+        tok = int(np.argmax(m.logits()[-1]))
+        tok_first = tok
+        barrier(pg)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            tok = m.eval_greedy(tok, 16 + (i % (n_ctx - 16)))
+        t1 = time.perf_counter()
+        barrier(pg)
+        el_g = all_max(pg, t1 - t0)
+        greedy = {"value": n_gpus * args.steps / el_g, "unit": "tok/s", "ms_per_step": el_g / args.steps * 1e3,
+                  "path": "lvk_eval_greedy: decode graph ending in the device argmax, 4-byte D2H",
+                  "first_token": tok_first}
+        # host sampler (llama_sample_top_p_top_k, main's defaults: top_k 40, top_p 0.95, temp 0.8,
+        # repeat_penalty 1.1 over a 64-token window) on the last logits
+        last64 = np.array(prompt_tokens(64), np.int32)
+        t0 = time.perf_counter()
+        for _ in range(200):
+            m.sample(last64, 40, 0.95, 0.8, 1.1)
+        greedy["host_sampler_us"] = (time.perf_counter() - t0) / 200 * 1e6
 
     # prompt eval: one 512-token batch (configs[2])
     p512 = np.array(prompt_tokens(512), np.int32)
