@@ -33,6 +33,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 MODEL_BYTES_7B = 4130490880    # algorithmic weight bytes per token
 MODEL_BYTES_13B_Q41 = 9640369920   # 13B Q4_1 weight bytes per token
+MODEL_BYTES_65B = 40644154368  # 65B Q4_0 weight bytes per token
+CFG_65B = dict(n_embd=8192, n_head=64, n_layer=80, ftype=2, seed=3)
 REF_PUBLISHED_TOKS = 16.3      # 7B Q4_0 predict 61.41 ms/token
 LAYER_MAT_WEIGHTS_7B = 32 * (4 * 4096 * 4096 + 3 * 4096 * 11008)   # weights of the 7B layer matrices
 VALU_FP32_TFLOPS = 157.3       # MI355X_MICROARCH.md: peak FP32 vector
@@ -94,33 +96,78 @@ def ensure_model(path, rank, pg, cfg):
     barrier(pg)
 
 
-def cpu_baseline(path, budget_s=15.0):
-    """Reference AVX2 ggml.c on the same file (oracle/_ref/libref.so)."""
+def cpu_info():
+    """host CPU facts for the baseline line: nproc, model, AVX flags,
+    physical cores of this process's CPU set"""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    try:
+        txt = open("/proc/cpuinfo").read()
+        for line in txt.splitlines():
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+        flags = next((l.split(":", 1)[1].split() for l in txt.splitlines() if l.startswith("flags")), [])
+        info["simd"] = [f for f in ("avx", "avx2", "fma", "f16c", "avx512f", "avx512bw") if f in flags]
+    except OSError:
+        pass
+    try:
+        out = subprocess.run(["lscpu", "-p=CPU,CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+        aff = os.sched_getaffinity(0)
+        cores = {(l.split(",")[2], l.split(",")[1]) for l in out.splitlines()
+                 if l and not l.startswith("#") and int(l.split(",")[0]) in aff}
+        info["physical_cores"] = len(cores)
+    except Exception:
+        info["physical_cores"] = None
+    return info
+
+
+def cpu_baseline(path, budget_s=20.0):
+    """The reference AVX2 ggml.c build (oracle/_ref/libref.so) on the same file and tokens:
+    decode tok/s best of 3 segments and the 512-token prompt batch, llama.cpp:1186-1195's
+    n_eval / t_eval and n_p_eval / t_p_eval."""
     from oracle_lib import REF_SO, Ref
     if not os.path.exists(REF_SO):
         return None
     import numpy as np
-    cores = min(16, len(os.sched_getaffinity(0)))
+    info = cpu_info()
+    # the reference is run at -t = physical cores, capped by this job's CPU share: the GPU
+    # box runs one job per GPU with OMP_NUM_THREADS (16) threads of its many cores
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0) or 16
+    threads = max(1, min(info.get("physical_cores") or info["affinity"], share))
     ref = Ref()
     m = ref.model(path, 512)
     toks = np.array(prompt_tokens(16), np.int32)
-    t0 = time.time()
-    lg = m.eval(toks, 0, n_threads=cores)
-    t_prompt = time.time() - t0
-    tok, n_past, n_dec, t_dec = int(np.argmax(lg[-1])), 16, 0, 0.0
-    while t_dec < budget_s and n_dec < 256:
-        t0 = time.time()
-        lg = m.eval(np.array([tok], np.int32), n_past, n_threads=cores)
-        t_dec += time.time() - t0
-        tok = int(np.argmax(lg[-1]))
-        n_past += 1
-        n_dec += 1
+    lg = m.eval(toks, 0, n_threads=threads)
+    tok, n_past = int(np.argmax(lg[-1])), 16
+    segs, seg_steps, t_used = [], 16, 0.0
+    for _ in range(3):                                       # best of 3 decode segments
+        t0 = time.perf_counter()
+        for _ in range(seg_steps):
+            lg = m.eval(np.array([tok], np.int32), n_past, n_threads=threads)
+            tok = int(np.argmax(lg[-1]))
+            n_past += 1
+        dt = time.perf_counter() - t0
+        segs.append(seg_steps / dt)
+        t_used += dt
+        if t_used > budget_s / 2:
+            break
+    p512 = np.array(prompt_tokens(512), np.int32)
+    pr = []
+    for _ in range(3):                                       # 512-token prompt batch, best of up to 3
+        t0 = time.perf_counter()
+        m.eval(p512, 0, n_threads=threads)
+        pr.append(512 / (time.perf_counter() - t0))
+        t_used += 512 / pr[-1]
+        if t_used > budget_s:
+            break
     m.close()
-    return {"value": n_dec / t_dec, "unit": "tok/s", "cores": cores, "kind": "reference",
-            "sample": "reference ggml.c AVX2 build (oracle/_ref), same synthetic 7B Q4_0 file, n_ctx 512, f16 KV: "
-                      "16-token prompt (%.2f s) then %d greedy decode steps (%.1f s), %d threads"
-                      % (t_prompt, n_dec, t_dec, cores),
-            "prompt_tok_s": 16 / t_prompt}
+    return {"value": max(segs), "unit": "tok/s", "cores": threads, "kind": "reference",
+            "sample": "reference ggml.c AVX2 build (oracle/_ref, compiled from the reference sources), the same "
+                      "synthetic 7B Q4_0 file and tokens, n_ctx 512, f16 KV, -t %d: 16-token prompt, then best of "
+                      "%d segments of %d greedy decode steps (positions 16..%d); prompt = one 512-token batch, "
+                      "best of %d" % (threads, len(segs), seg_steps, n_past - 1, len(pr)),
+            "decode_segments_tok_s": segs, "prompt_tok_s": max(pr), "prompt_runs_tok_s": pr,
+            "host": info}
 
 
 def layer_split_decode(args, m_full, rank, ws, local, pg, n_ctx, ptoks):
@@ -169,6 +216,49 @@ def layer_split_decode(args, m_full, rank, ws, local, pg, n_ctx, ptoks):
             "ms_per_token": dt / args.steps_split * 1e3}
 
 
+def decode_65b(args, rank, pg, n_ctx, ptoks):
+    """LLaMA-65B Q4_0 single-stream decode on ONE GPU (BASELINE configs[4] at S = 1: the
+    40.6 GB of weights fit in 288 GB of HBM): tok/s, fraction of the model-bytes roofline
+    (197 tok/s at 8 TB/s) and a per-kernel-class profile"""
+    import numpy as np
+    import lvk
+    path = os.path.join(os.path.dirname(args.model), "llama-65b-q4_0.bin")
+    t0 = time.time()
+    ensure_model(path, rank, pg, CFG_65B)
+    gen_s = time.time() - t0
+    t0 = time.time()
+    m = lvk.Llama(path, n_ctx=n_ctx)
+    load_s = time.time() - t0
+    lg = m.eval(ptoks, 0)
+    tok = int(np.argmax(lg[-1]))
+    for i in range(4):
+        tok = int(np.argmax(m.eval([tok], 16 + i)[-1]))
+    barrier(pg)
+    t0 = time.perf_counter()
+    for i in range(args.steps_65b):
+        tok = int(np.argmax(m.eval([tok], 16 + (i % (n_ctx - 16)))[-1]))
+    dt = all_max(pg, time.perf_counter() - t0)
+    r = args.steps_65b / dt
+    m.set_profiling(True)
+    m.reset_profile()
+    for i in range(8):
+        tok = int(np.argmax(m.eval([tok], 16 + i * 60)[-1]))
+    prof = m.profile()
+    m.set_profiling(False)
+    m.close()
+    kernels = {k: {"avg_us": v["ms"] / v["launches"] * 1e3,
+                   "gbs": (v["bytes"] / v["launches"]) / (v["ms"] / v["launches"] * 1e-3) / 1e9 if v["bytes"] else None}
+               for k, v in prof.items() if v["launches"]}
+    return {"value": r, "unit": "tok/s", "steps": args.steps_65b, "ms_per_token": 1e3 / r,
+            "workload": "LLaMA-65B Q4_0 (synthetic, seed 3; n_embd 8192, 64 heads, 80 layers, n_ff 22016) "
+                        "single-stream greedy decode on 1 GPU, positions 16..%d, n_ctx %d"
+                        % (16 + min(args.steps_65b, n_ctx - 16) - 1, n_ctx),
+            "model_bytes_per_token": MODEL_BYTES_65B,
+            "frac_hbm_roofline": r * MODEL_BYTES_65B / 1e9 / HBM_PEAK_GBS,
+            "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_65B,
+            "kernels": kernels, "gen_s": gen_s, "load_s": load_s}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None)
@@ -182,12 +272,14 @@ def main():
                     help="skip the lvk_eval_greedy decode leg (rocprofv3 kernel-trace runs, DESIGN.md section 9)")
     ap.add_argument("--no-13b", action="store_true", help="skip the 13B Q4_1 decode line (BASELINE configs[3])")
     ap.add_argument("--steps-13b", type=int, default=96)
+    ap.add_argument("--no-65b", action="store_true", help="skip the 1-GPU 65B decode line (BASELINE configs[4], S=1)")
+    ap.add_argument("--steps-65b", type=int, default=32)
     ap.add_argument("--no-split", action="store_true", help="N>1: skip the layer-split pipeline line (SURVEY 8e)")
     ap.add_argument("--steps-split", type=int, default=64)
     ap.add_argument("--split-model", default=None, help="model for the layer-split line (default: the 7B file)")
     ap.add_argument("--split-backend", default="nccl", choices=["nccl", "gloo"],
                     help="stage hand-off transport: RCCL on device buffers, or gloo through host memory")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
     args = ap.parse_args()
 
@@ -227,6 +319,8 @@ def main():
     barrier(pg)
     elapsed = all_max(pg, t1 - t0)
     value = n_gpus * args.steps / elapsed
+    last = 16 + min(args.steps, n_ctx - 16) - 1
+    positions = "16..%d" % last + ("" if args.steps <= n_ctx - 16 else " (wrapping to 16 after 511)")
 
     greedy = None
     if not args.no_greedy:
@@ -246,7 +340,8 @@ def main():
                   "path": "lvk_eval_greedy: decode graph ending in the device argmax, 4-byte D2H",
                   "first_token": tok_first}
         # host sampler (llama_sample_top_p_top_k, main's defaults: top_k 40, top_p 0.95, temp 0.8,
-        # repeat_penalty 1.1 over a 64-token window) on the last logits
+        # repeat_penalty 1.1 over a 64-token window) on fresh logits (lvk_eval_greedy leaves none)
+        m.eval([tok], 16)
         last64 = np.array(prompt_tokens(64), np.int32)
         t0 = time.perf_counter()
         for _ in range(200):
@@ -320,9 +415,9 @@ def main():
         split = layer_split_decode(args, m, rank, ws, local, pg, n_ctx, ptoks)
 
     # 13B Q4_1 single-stream decode (BASELINE.json configs[3]), same loop
+    m.close()          # one model resident at a time from here on
     q41 = None
     if not args.no_13b:
-        m.close()
         path13 = os.path.join(os.path.dirname(args.model), "llama-13b-q4_1.bin")
         ensure_model(path13, rank, pg, dict(n_embd=5120, n_head=40, n_layer=40, ftype=3, seed=2))
         m13 = lvk.Llama(path13, n_ctx=n_ctx)
@@ -344,10 +439,11 @@ def main():
                "model_bytes_per_token": MODEL_BYTES_13B_Q41,
                "frac_hbm_roofline": r13 * MODEL_BYTES_13B_Q41 / 1e9 / HBM_PEAK_GBS,
                "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_13B_Q41}
+    d65 = None
+    if ws == 1 and not args.no_65b:
+        d65 = decode_65b(args, rank, pg, n_ctx, ptoks)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        if args.no_13b:
-            m.close()
         cpu = cpu_baseline(args.model, args.cpu_budget)
 
     if rank == 0:
@@ -358,8 +454,9 @@ def main():
             "scaling": "weak", "vs_baseline": value / REF_PUBLISHED_TOKS,
             "dtype": "i4xi4->f32 (Q4_0 blocks, exact int dots, fp32 FMA chains)",
             "data": "synthetic (seeded ggjt 7B Q4_0, lvk-gen-model seed 1)",
-            "config": {"workload": "LLaMA-7B Q4_0 single-stream decode: 16-token prompt then greedy decode over "
-                                   "positions 16..511, n_ctx 512, f16 KV", "n_ctx": n_ctx,
+            "config": {"workload": "LLaMA-7B Q4_0 single-stream decode: 16-token prompt then %d greedy decode "
+                                   "steps at positions %s, n_ctx 512, f16 KV" % (args.steps, positions),
+                       "n_ctx": n_ctx,
                        "parallelism": "replicas" if n_gpus > 1 else "single-gpu"},
             "roofline": roofline,
             "step_roofline": {"model_bytes_per_token": MODEL_BYTES_7B, "achieved_gbs": step_gbs,
@@ -367,6 +464,7 @@ def main():
             "prompt_eval": prompt,
             "decode_greedy_device": greedy,
             "decode_13b_q4_1": q41,
+            "decode_65b_q4_0": d65,
             "layer_split": split,
             "kernels": kernels,
             "cpu_baseline": cpu,

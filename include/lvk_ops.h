@@ -42,11 +42,11 @@ LVK_API int lvk_mul_mat_q_norm(int type, const void * w, int m, int k, const flo
 
 /* The prompt-batch (N > 1) matmul on the MFMA cores (mm_mfma.hip), Q4_0 only:
  * same inputs and meaning as lvk_mul_mat_q / lvk_mul_mat_q_norm (g != NULL:
- * fused RMSNorm * g).  The activation quantization and every per-block
- * integer dot are bit-exact; the block scales are accumulated in fp32 in block
- * order, acc = fmaf(dw*dx, I_b, acc), instead of the reference's 8 interleaved
- * AVX2 chains (ggml.c:1950-2026), so results agree with lvk_mul_mat_q to fp32
- * rounding.  Needs m % 128 == 0, k % 256 == 0, n >= 1. */
+ * fused RMSNorm * g), and the same result bits: the matrix cores produce each
+ * AVX2 chain's exact 4-element integer partial and the f32 scale products
+ * dw*dx (one rounding each), and the VALU runs the reference's 8 fp32 chains
+ * and horizontal order (ggml.c:1950-2026).  Needs m % 128 == 0, k % 256 == 0,
+ * n >= 1. */
 LVK_API int lvk_mul_mat_q_mfma(int type, const void * w, int m, int k, const float * g, const float * x, int n,
                                float * y);
 

@@ -76,13 +76,24 @@ __device__ __forceinline__ float quad_reduce(const float s[8]) {
 typedef unsigned long long u64g __attribute__((address_space(1)));
 typedef unsigned u32g __attribute__((address_space(1)));
 
+#ifndef LVK_SPIN_LIMIT   // probe builds may lower it to exercise the timeout path
+#define LVK_SPIN_LIMIT (1 << 22)
+#endif
+
+// a spin that gave up: the error word (host-mapped, lvk_kernels.h LVK_ERR_*) tells
+// the host, which fails the eval instead of returning wrong numbers
+__device__ __forceinline__ void raise_error(unsigned * err, unsigned code) {
+    if (err) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // relaxed agent-scope poll of one granule until it carries `epoch`; bounded so a
-// violated residency assumption ends in wrong numbers, never in a hung GPU
-__device__ __forceinline__ unsigned long long poll_granule(u64g * p, unsigned epoch) {
+// violated residency assumption can never hang the GPU -- it raises the error word
+__device__ __forceinline__ unsigned long long poll_granule(u64g * p, unsigned epoch, unsigned * err) {
     unsigned long long x;
     for (int spins = 0;; ++spins) {
         x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((unsigned) (x >> 32) == epoch || spins > (1 << 22)) break;
+        if ((unsigned) (x >> 32) == epoch) break;
+        if (spins > LVK_SPIN_LIMIT) { raise_error(err, LVK_ERR_ATTN_SPIN); break; }
         __builtin_amdgcn_s_sleep(1);
     }
     return x;
@@ -114,6 +125,7 @@ struct AttnDArgs {
     ActQ out;
     float * out_f32;
     int exp_mode;
+    unsigned * err;               // host-mapped error word (nullptr: none)
 };
 
 // EXCH: the 4 workgroups of a head split the scores and exchange them as granules;
@@ -130,22 +142,15 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     u64g * g = (u64g *) (A.gran + (size_t) h * n_ctx);
     LVK_DT(0);
 
-    // 1a. loads that do not depend on n_past go out before the step block is read (its
-    // load is a full memory round trip): Q, the K rows of this workgroup's first two
-    // 64-position chunks and the first 512 positions of its 32 V rows (addresses inside
-    // the caches; positions past n_kv are never used)
+    // 1a. Q and the step block go out together (one memory round trip); every K and V
+    // load is bounded by n_kv, so a launch reads exactly the positions it uses
     const uint4 * qp = (const uint4 *) (A.q16 + h * HD) + r;
     uint4 qv[4];
 #pragma unroll
     for (int st = 0; st < 4; ++st) qv[st] = qp[st * 4];
-    uint4 kv[2][4];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const int p = min((EXCH ? sl * 64 + c * 256 : c * 64) + (tid >> 2), n_ctx - 1);
-        const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
-#pragma unroll
-        for (int st = 0; st < 4; ++st) kv[c][st] = kp[st * 4];
-    }
+    const int n_kv = A.sp->n_past + 1;
+    const int n_pad = (n_kv + 31) & ~31;
+    const int np = n_kv & ~31;
     auto v_dma = [&](int p0, int lim) {             // positions [p0, p0 + 512) of the 32 rows, below lim
         for (int row = wave; row < 32; row += 4)
             if (p0 + lane * 8 < lim)
@@ -153,13 +158,17 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
                                                  (__attribute__((address_space(3))) void *) (vl + (size_t) row * n_ctx + p0),
                                                  16, 0, 0);
     };
+    uint4 kv[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int p = min((EXCH ? sl * 64 + c * 256 : c * 64) + (tid >> 2), n_kv - 1);
+        const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) kv[c][st] = kp[st * 4];
+    }
     LVK_DT(6);
-    v_dma(0, min(n_ctx, 512));
+    for (int p0 = 0; p0 < n_pad; p0 += 512) v_dma(p0, n_pad);
     LVK_DT(7);
-    const int n_kv = A.sp->n_past + 1;
-    const int n_pad = (n_kv + 31) & ~31;
-    const int np = n_kv & ~31;
-    for (int p0 = 512; p0 < n_pad; p0 += 512) v_dma(p0, n_pad);
     LVK_DT(1);
 
     // 1b. scores of chunks sl, sl+4, ... (one position per lane quad)
@@ -180,6 +189,9 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
             if (r == 0 && p < n_kv) {
                 const float v = kq * A.scale;                    // ggml_vec_scale_f32 (llama.cpp:1026)
                 if constexpr (!EXCH) sc[p] = v;
+#ifdef LVK_PROBE_DROP_GRANULE   // fault-injection probe build only: position 0's score is never published
+                else if (p == 0) {}
+#endif
                 else __hip_atomic_store(g + p, ((unsigned long long) A.epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -203,7 +215,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     float mx = -INFINITY;
     if constexpr (!EXCH) __syncthreads();
     for (int p = tid; p < n_kv; p += 256) {
-        const float v = EXCH ? __uint_as_float((unsigned) poll_granule(g + p, A.epoch)) : sc[p];
+        const float v = EXCH ? __uint_as_float((unsigned) poll_granule(g + p, A.epoch, A.err)) : sc[p];
         sc[p] = v;
         mx = v > mx ? v : mx;
     }
@@ -350,7 +362,8 @@ struct WoArgs {
 };
 
 __device__ __forceinline__ void wo_run(const WoArgs & P, unsigned long long * ogran, unsigned * ocount,
-                                       const unsigned target, const unsigned epoch, const int b, uint8_t * smem) {
+                                       const unsigned target, const unsigned epoch, const int b, uint8_t * smem,
+                                       unsigned * err) {
     using namespace wo;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -400,10 +413,11 @@ __device__ __forceinline__ void wo_run(const WoArgs & P, unsigned long long * og
             __builtin_amdgcn_s_sleep(127);
             __builtin_amdgcn_s_sleep(127);
         }
-        for (int spins = 0; __hip_atomic_load((u32g *) ocount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-                            spins < (1 << 20);
-             ++spins)
+        for (int spins = 0; __hip_atomic_load((u32g *) ocount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;
+             ++spins) {
+            if (spins > (LVK_SPIN_LIMIT >> 2)) { raise_error(err, LVK_ERR_ATTN_SPIN); break; }
             __builtin_amdgcn_s_sleep(LVK_PROBE_WO_MODE == 3 ? 4 : 16);
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");     // no granule load above the wait
     if constexpr (LVK_PROBE_WO_MODE == 2) {
@@ -418,7 +432,7 @@ __device__ __forceinline__ void wo_run(const WoArgs & P, unsigned long long * og
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
         const int i = lane + 64 * k;
-        const unsigned word = (unsigned) ((unsigned) (gv[k] >> 32) == epoch ? gv[k] : poll_granule(og + i, epoch));
+        const unsigned word = (unsigned) ((unsigned) (gv[k] >> 32) == epoch ? gv[k] : poll_granule(og + i, epoch, err));
         const int blk = i / 5, k5 = i - blk * 5;
         if (k5 == 0) dxp[(blk >> 5) * 32 + (blk & 7) * 4 + ((blk >> 3) & 3)] = __uint_as_float(word);
         else mv::act_store(act, dxp, blk, k5 - 1, word, 0.0f, false);
@@ -484,7 +498,7 @@ __global__ __launch_bounds__(256) void k_attn_wo(AttnDArgs A, WoArgs P) {
     // slices of a head on one XCD as in k_attn_d's (H, 4) grid), then the Wo workgroups
     const int nattn = (int) gridDim.x - P.nwg;
     if (b < nattn) attn_d_run<Q4_0>(A, (b & 7) + 8 * (b >> 5), (b >> 3) & 3, smem);
-    else wo_run(P, A.ogran, A.ocount, (unsigned) nattn * A.epoch, A.epoch, b - nattn, smem);
+    else wo_run(P, A.ogran, A.ocount, (unsigned) nattn * A.epoch, A.epoch, b - nattn, smem, A.err);
 }
 
 int n_cus() {
@@ -518,6 +532,7 @@ AttnDArgs attn_args(const AttnLaunch & A, void * gran, unsigned epoch) {
     a.out = A.out;
     a.out_f32 = A.out_f32;
     a.exp_mode = A.exp_computed;
+    a.err = A.err;
     return a;
 }
 

@@ -38,6 +38,11 @@ struct EventSplit {
 
 enum QType : int { Q4_0 = 2, Q4_1 = 3 };
 
+// error word: kernels whose workgroups wait on each other spin with a bound; a
+// spin that gives up stores one of these into the context's host-mapped error
+// word (system scope) instead of hanging, and the host fails the eval
+enum DevError : unsigned { LVK_ERR_NONE = 0, LVK_ERR_ATTN_SPIN = 1, LVK_ERR_DECODE_SPIN = 2 };
+
 // ---------------------------------------------------------------------------
 // Device weight image of one quantized matrix W[M][K] (ggml row-major, K = row
 // length) in the "octet" layout: rows are grouped 8 per
@@ -133,6 +138,7 @@ struct AttnLaunch {
     float * out_f32 = nullptr; // optional: also store the unquantized merged heads [N][E]
     uint16_t * p16_out = nullptr; // optional (debug): f16 probabilities [N][H][n_ctx]
     int exp_computed = 0;     // exp mode (lvk_device.h exp_f16): 0 table, 1 double, 2 f32 -- nonzero only after exp_check
+    unsigned * err = nullptr; // host-mapped error word (DevError); kernels that spin report a timeout here
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
 // prompt batches (N > 1, Q4_0 output): scores+softmax per (head, 32 tokens) then

@@ -436,7 +436,9 @@ hipError_t go(const CuParams & P, hipStream_t s) {
 #ifdef LVK_PROBE_TIMING
 void * lvk_probe_trace() { void * p = nullptr; (void) hipGetSymbolAddress(&p, HIP_SYMBOL(g_trace)); return p; }
 #endif
-bool matvec_cu_supported(int K) { return K == 4096 || K == 11008; }
+// row lengths compiled in: the LLaMA 7B/13B-free Q4_0 shapes (n_embd 4096 / 8192,
+// n_ff 11008 / 22016; llama.cpp:771-779)
+bool matvec_cu_supported(int K) { return K == 4096 || K == 11008 || K == 8192 || K == 22016; }
 
 hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s) {
     if (L.w.qtype != Q4_0 || L.n_tokens != 1 || L.w.M % 8) return hipErrorNotSupported;
@@ -469,6 +471,9 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(4, 0, 4), C3(4, 0, 11), C3(2, 0, 11), C3(4, 0, 8))
     }
 #endif
+    // launch shapes (waves NW, prefetch depth D) per row length and role, measured on
+    // the 7B shapes (tools/probe, LVK_PROBE_SWEEP) and scaled for 65B: enough waves that
+    // every CU keeps ~60-120 KB of weights in flight
     if (K == 4096) {
         switch (epi) {
             case EPI_QKV: if (pro == PRO_NORM) return go<8, 0, 2, PRO_NORM, EPI_QKV, 4096>(P, s); break;
@@ -478,10 +483,22 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         }
         // operator API (lvk_mul_mat_q: plain quantize of an f32 input)
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 4096>(P, s);
+    } else if (K == 8192) {
+        switch (epi) {
+            case EPI_QKV: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_QKV, 8192>(P, s); break;
+            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 8192>(P, s); break;
+            case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 8192>(P, s); break;
+            case EPI_RESID: if (pro == PRO_ACTQ) return go<4, 0, 2, PRO_ACTQ, EPI_RESID, 8192>(P, s); break;
+        }
+        if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 8192>(P, s);
     } else if (K == 11008) {
         if (epi == EPI_RESID && pro == PRO_ACTF) return go<4, 0, 4, PRO_ACTF, EPI_RESID, 11008>(P, s);
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 0, 4, PRO_ACTF, EPI_STORE, 11008>(P, s);
         if (epi == EPI_STORE && pro == PRO_NORM) return go<4, 0, 4, PRO_NORM, EPI_STORE, 11008>(P, s);
+    } else if (K == 22016) {
+        if (epi == EPI_RESID && pro == PRO_ACTF) return go<4, 0, 2, PRO_ACTF, EPI_RESID, 22016>(P, s);
+        if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 0, 2, PRO_ACTF, EPI_STORE, 22016>(P, s);
+        if (epi == EPI_STORE && pro == PRO_NORM) return go<4, 0, 2, PRO_NORM, EPI_STORE, 22016>(P, s);
     }
     return hipErrorNotSupported;
 }

@@ -94,6 +94,12 @@ std::vector<int> tokenize(const lvk::Vocab & vocab, const std::string & text, bo
 int sample_top_p_top_k(lvk::Context & c, const std::vector<int> & last, int top_k, float top_p, float temp,
                        float repeat_penalty) {
     const int n_logits = (int) c.model.hp.n_vocab;
+    if (!c.logits_valid || c.logits.size() < (size_t) n_logits) {
+        // no eval has left host logits (none yet, a failed eval, or lvk_eval_greedy, which
+        // keeps them on the device): nothing to sample from
+        fprintf(stderr, "llama_sample_top_p_top_k: no logits (call llama_eval first)\n");
+        return -1;
+    }
     const float * pl = c.logits.data() + c.logits.size() - n_logits;
     if (temp <= 0) {
         float best = pl[0];

@@ -68,6 +68,7 @@ Context::~Context() {
     for (auto & e : ev_pool) { (void) hipEventDestroy(e.first); (void) hipEventDestroy(e.second); }
     if (sp_h) (void) hipHostFree(sp_h);
     if (tok_h) (void) hipHostFree(tok_h);
+    if (err_h) (void) hipHostFree(err_h);
     if (stream) (void) hipStreamDestroy(stream);
 }
 
@@ -113,6 +114,10 @@ void Context::init(const llama_context_params & p) {
     tok_d = (int *) model.alloc(C * 4);
     LVK_HIP(hipHostMalloc((void **) &sp_h, sizeof(StepParams), hipHostMallocDefault));
     LVK_HIP(hipHostMalloc((void **) &tok_h, C * 4, hipHostMallocDefault));
+    LVK_HIP(hipGetDevice(&device));
+    LVK_HIP(hipHostMalloc((void **) &err_h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    *err_h = 0;
+    LVK_HIP(hipHostGetDevicePointer((void **) &err_d, err_h, 0));
     greedy_d = (int *) model.alloc(4);
     LVK_HIP(hipHostMalloc((void **) &greedy_h, 4, hipHostMallocDefault));
 
@@ -138,6 +143,15 @@ void Context::init(const llama_context_params & p) {
     LVK_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     logits.reserve(logits_all ? C * V : V);
     if (want_embedding) embedding.resize(E);
+}
+
+void Context::check_device_error() {
+    const unsigned e = __atomic_load_n(err_h, __ATOMIC_ACQUIRE);
+    if (e == LVK_ERR_NONE) return;
+    __atomic_store_n(err_h, 0u, __ATOMIC_RELEASE);
+    logits_valid = false;
+    throw Error(e == LVK_ERR_ATTN_SPIN ? "llama.vk_amd: decode attention: a workgroup wait timed out (results discarded)"
+                                       : "llama.vk_amd: persistent decode: a phase wait timed out (results discarded)");
 }
 
 void Context::timed_launch(int cls, double bytes, const std::function<hipError_t()> & fn) {
@@ -218,6 +232,7 @@ void Context::enqueue_forward(int n, bool last_only) {
             });
             AttnLaunch at{q16, kcl, vcl, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
             at.exp_computed = exp_computed;
+            at.err = err_d;
             if (attention_prompt_supported(E, H, n_ctx)) {
                 // writes the Wo input in both forms (ActQ and the MFMA fragment image)
                 timed_launch(K_ATTN, 0, [&] {
@@ -279,6 +294,7 @@ void Context::enqueue_forward(int n, bool last_only) {
         timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
         AttnLaunch at{q16, kc + il * CE, vc + il * CE, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
         at.exp_computed = exp_computed;
+        at.err = err_d;
         if (attn_wo) {
             timed_launch(K_ATTN_WO, qbytes(ly.wo), [&] {
                 return launch_attention_wo(at, ly.wo, x, attn_gran, (unsigned) il + 1, stream);
@@ -369,6 +385,8 @@ int Context::eval_greedy(int token, int n_past) {
     }
     LVK_HIP(hipStreamSynchronize(stream));
     if (profiling) collect_profile();
+    check_device_error();
+    logits_valid = false;     // llama_get_logits still holds an earlier eval's row
     return *greedy_h;
 }
 
@@ -405,6 +423,8 @@ void Context::eval(const int * tokens, int n, int n_past) {
     }
     LVK_HIP(hipStreamSynchronize(stream));
     if (profiling) collect_profile();
+    check_device_error();
+    logits_valid = model.has_head;
 }
 
 size_t Context::kv_bytes() const {
@@ -431,8 +451,14 @@ void Context::kv_set(const uint8_t * src, size_t n) {
 // (layer, dim).  Only the n_tokens positions move, not the whole cache.
 void Context::kv_copy_from(const Context & src, int n_tokens) {
     const size_t E = model.hp.n_embd, L = model.layers.size(), C = (size_t) n_ctx;
-    if (src.model.hp.n_embd != model.hp.n_embd || src.model.layers.size() != L || src.n_ctx != n_ctx)
-        throw Error("lvk_kv_copy: contexts differ in n_embd, n_layer or n_ctx");
+    if (src.model.hp.n_embd != model.hp.n_embd || src.model.layers.size() != L || src.n_ctx != n_ctx ||
+        src.model.hp.n_head != model.hp.n_head || src.model.layer_begin != model.layer_begin)
+        throw Error("lvk_kv_copy: contexts differ in n_embd, n_head, n_layer, layer range or n_ctx");
+    if (src.device != device) throw Error("lvk_kv_copy: contexts live on different HIP devices");
+    // the K/V bytes are only meaningful under the weights that wrote them: same model
+    // file contents (size and quantization type are checked; the caller owns identity)
+    if (src.model.qtype != model.qtype || src.model.file_bytes != model.file_bytes)
+        throw Error("lvk_kv_copy: contexts hold different models");
     if (n_tokens < 0 || n_tokens > n_ctx) throw Error("lvk_kv_copy: n_tokens out of range");
     if (n_tokens > 0) {
         const size_t n = (size_t) n_tokens;

@@ -67,6 +67,9 @@ struct Context {
     int * tok_d = nullptr;       // [n_ctx]
     StepParams * sp_h = nullptr; // pinned
     int * tok_h = nullptr;       // pinned
+    unsigned * err_h = nullptr;  // pinned, mapped: the kernels' error word (lvk_kernels.h DevError)
+    unsigned * err_d = nullptr;  // its device address
+    int device = 0;              // the HIP device of this context
 
     // prompt (N > 1) path: MFMA matmuls with exact block dots (default) or the
     // bit-faithful VALU kernels (prompt_exact; env LVK_PROMPT_EXACT=1)
@@ -93,6 +96,7 @@ struct Context {
 
     // host-visible results
     std::vector<float, PinnedAlloc<float>> logits;
+    bool logits_valid = false;   // false after lvk_eval_greedy (host logits not refreshed) or a failed eval
     std::vector<float> embedding;
     std::vector<uint8_t> kv_host;
     int kv_n = 0;
@@ -125,6 +129,8 @@ struct Context {
     size_t kv_bytes() const;
     void timed_launch(int cls, double bytes, const std::function<hipError_t()> & fn);
     void collect_profile();
+    // after a stream sync: throw if a kernel raised the error word (and clear it)
+    void check_device_error();
 };
 
 int64_t now_us();

@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libllama_vk_amd.so")
+# LVK_LIB selects another build of the same library (the fault-injection probe build, tests only)
+LIB_PATH = os.environ.get("LVK_LIB") or os.path.join(HERE, "lib", "libllama_vk_amd.so")
 GEN_BIN = os.path.join(HERE, "bin", "lvk-gen-model")
 
 if not os.path.exists(LIB_PATH):

@@ -46,6 +46,7 @@ def ref():
 TINY = {
     "tiny_q4_0": dict(n_embd=256, n_head=2, n_layer=32, ftype=2, seed=1),
     "tiny_q4_1": dict(n_embd=256, n_head=2, n_layer=40, ftype=3, seed=7),
+    "tiny_l80_q4_0": dict(n_embd=256, n_head=2, n_layer=80, ftype=2, seed=3),
 }
 
 

@@ -13,6 +13,7 @@ Outputs (tests/golden/):
                      --n-embd 256 --n-head 2 --n-layer 32 --seed 1) for a chunked
                      16+8+24-token prompt then 6 greedy decode steps (main-style)
   tiny_q4_1.npz      same for the tiny 40-layer Q4_1 model (--ftype 3 --seed 7)
+  tiny_l80_q4_0.npz  same for an 80-layer Q4_0 model (the reference's 65B layer count, --seed 3)
   test_quantize.json known answers of the reference's tests/test-quantize.c
 """
 import hashlib
@@ -29,6 +30,8 @@ from oracle_lib import Ref, gen_model, prompt_tokens  # noqa: E402
 TINY = {
     "tiny_q4_0": dict(n_embd=256, n_head=2, n_layer=32, ftype=2, seed=1),
     "tiny_q4_1": dict(n_embd=256, n_head=2, n_layer=40, ftype=3, seed=7),
+    # 80 layers: the reference's MODEL_65B branch (llama.cpp:778) on a model small enough for a fixture
+    "tiny_l80_q4_0": dict(n_embd=256, n_head=2, n_layer=80, ftype=2, seed=3),
 }
 CHUNKS = (16, 8, 24)
 N_DECODE = 6
@@ -106,11 +109,16 @@ def tiny(ref, name, cfg, tmp):
 
 def main():
     ref = Ref()
-    ops(ref)
+    only = sys.argv[1:]          # optional: regenerate only these fixtures (names without .npz)
+    if not only:
+        ops(ref)
     tmp = "/tmp/lvk_golden"
     os.makedirs(tmp, exist_ok=True)
     for name, cfg in TINY.items():
-        tiny(ref, name, cfg, tmp)
+        if not only or name in only:
+            tiny(ref, name, cfg, tmp)
+    if only:
+        return
     # reference tests/test-quantize.c known answers (src[i] = i+1)
     src = np.arange(1, 33, dtype=np.float32)
     q0 = ref.quantize(src, 2, reference=True)

@@ -56,12 +56,14 @@ def test_dropin_main_greedy_text_matches_reference_cpu(tiny_models):
     _need(REF_MAIN)
     args = ["-m", tiny_models["tiny_q4_0"], "-p", "Building a website can be done in 10 simple steps:",
             "-n", "48", "--temp", "0", "-s", "1", "-c", "256", "--ignore-eos"]
-    # bit-exact prompt batches (the default MFMA prompt path agrees to fp32 rounding only)
+    # both prompt paths are bit-exact: the default MFMA matmuls and the VALU kernels
+    gpu_out, gpu_err = _run([exe] + args + ["-t", "1"])
     os.environ["LVK_PROMPT_EXACT"] = "1"
     try:
-        gpu_out, gpu_err = _run([exe] + args + ["-t", "1"])
+        exact_out, _ = _run([exe] + args + ["-t", "1"])
     finally:
         del os.environ["LVK_PROMPT_EXACT"]
+    assert exact_out == gpu_out
     cpu_out, _ = _run([REF_MAIN] + args + ["-t", "8"])
     assert gpu_out == cpu_out
     assert len(gpu_out) > 60
@@ -98,7 +100,4 @@ def test_dropin_perplexity_matches_reference_cpu(tiny_models, tmp_path):
         del os.environ["LVK_PROMPT_EXACT"]
     assert _ppl_values(exact_out) == want        # bit-exact logits -> the same printed digits
     mfma_out, _ = _run([exe] + args + ["-t", "1"])
-    got = _ppl_values(mfma_out)
-    assert [i for i, _ in got] == [i for i, _ in want]
-    for (_, a), (_, b) in zip(got, want):
-        assert abs(a - b) <= 1e-3 * b
+    assert _ppl_values(mfma_out) == want         # the MFMA prompt path is bit-exact too

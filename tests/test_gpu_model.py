@@ -24,7 +24,8 @@ def lvk(gpu_available):
     return m
 
 
-@pytest.mark.parametrize("name,graph", [("tiny_q4_0", True), ("tiny_q4_0", False), ("tiny_q4_1", True)])
+@pytest.mark.parametrize("name,graph", [("tiny_q4_0", True), ("tiny_q4_0", False), ("tiny_q4_1", True),
+                                        ("tiny_l80_q4_0", True)])
 def test_tiny_matches_reference_golden(lvk, tiny_models, name, graph):
     g = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
     m = lvk.Llama(tiny_models[name], n_ctx=512)
@@ -219,6 +220,61 @@ def test_mfma_prompt_7b_shaped_vs_oracle(lvk, oracle, model_dir):
     assert np.array_equal(bits(a), bits(b))
     n_past, tok = len(toks), int(np.argmax(b[-1]))
     for _ in range(4):
+        a = m.eval([tok], n_past)
+        b = om.eval([tok], n_past)
+        assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past
+        n_past += 1
+        tok = int(np.argmax(b[-1]))
+    m.close()
+    om.close()
+
+
+# ---------------------------------------------------------------------------
+# LLaMA-65B layer shapes (n_embd 8192, 64 heads, n_ff 22016; llama.cpp:771-778):
+# the decode kernels compiled for K = 8192 / 22016, the 64-head attention grid
+# (256 workgroups exchanging score granules) and the MFMA prompt matmuls.
+# ---------------------------------------------------------------------------
+def _model_65b_l2(model_dir):
+    from oracle_lib import gen_model
+    return gen_model(os.path.join(model_dir, "w8192_l2.bin"), n_embd=8192, n_head=64, n_layer=2, ftype=2, seed=13)
+
+
+def test_65b_shaped_decode_vs_oracle(lvk, oracle, model_dir):
+    path = _model_65b_l2(model_dir)
+    m = lvk.Llama(path, n_ctx=512)
+    m.set_prompt_exact(True)
+    om = oracle.model(path, 512)
+    toks = np.array([1, 450, 4996, 17354, 1701, 29916, 338, 263], np.int32)
+    a = m.eval(toks, 0)
+    b = om.eval(toks, 0)
+    assert np.array_equal(bits(a), bits(b))
+    n_past, tok = len(toks), int(np.argmax(a[-1]))
+    for _ in range(30):          # crosses the 32-position f16-dot tail boundary
+        a = m.eval([tok], n_past)
+        b = om.eval([tok], n_past)
+        assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past
+        n_past += 1
+        tok = int(np.argmax(a[-1]))
+    m.set_profiling(True)
+    m.reset_profile()
+    m.eval([tok], n_past)
+    pr = m.profile()
+    assert pr["qkv"]["launches"] == 2 and pr["w2"]["launches"] == 2
+    m.close()
+    om.close()
+
+
+def test_mfma_prompt_65b_shaped_vs_oracle(lvk, oracle, model_dir):
+    """a 72-token prompt (ragged token tile) through the MFMA matmuls at K = 8192 / 22016, then decode"""
+    path = _model_65b_l2(model_dir)
+    m = lvk.Llama(path, n_ctx=256)
+    om = oracle.model(path, 256)
+    toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 72)], np.int32)
+    a = m.eval(toks, 0)
+    b = om.eval(toks, 0)
+    assert np.array_equal(bits(a), bits(b))
+    n_past, tok = len(toks), int(np.argmax(b[-1]))
+    for _ in range(8):
         a = m.eval([tok], n_past)
         b = om.eval([tok], n_past)
         assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past

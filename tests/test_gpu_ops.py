@@ -43,7 +43,8 @@ def _oracle_mm(oracle, wq, xq_rows, k, qt):
     return np.array([[oracle.vec_dot(qt, k, wr, xr) for wr in wq] for xr in xq_rows], np.float32)
 
 
-@pytest.mark.parametrize("m,k,n", [(64, 256, 1), (48, 4096, 1), (32, 11008, 1), (64, 4096, 5), (16, 4096, 9)])
+@pytest.mark.parametrize("m,k,n", [(64, 256, 1), (48, 4096, 1), (32, 11008, 1), (64, 4096, 5), (16, 4096, 9),
+                                   (40, 8192, 1), (24, 22016, 1)])
 def test_mul_mat_q4_0(lvk, oracle, m, k, n):
     rng = np.random.default_rng(m * 7 + k + n)
     wq = _weights(oracle, rng, m, k, 2)
@@ -151,6 +152,21 @@ def test_attention_decode_kernels(lvk, oracle, monkeypatch, exp_path, n_past, C,
     kc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
     vc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
     q = (qs * rng.standard_normal(E)).astype(np.float32)
+    got = lvk.attention_decode(kc, vc, q, E, H, C, n_past)
+    want = np.zeros(E, np.float32)
+    oracle.lib.orc_attention(kc, vc, q, E, H, C, n_past, 1, want)
+    assert np.array_equal(bits(got), bits(want))
+
+
+@pytest.mark.parametrize("n_past", [0, 37, 300, 511])
+def test_attention_decode_65b_heads(lvk, oracle, n_past):
+    """LLaMA-65B attention shape: 64 heads x 128 (grid 64 x 4 = 256 workgroups exchanging
+    score granules), bit-identical to the reference graph"""
+    E, H, C = 8192, 64, 512
+    rng = np.random.default_rng(n_past + 65)
+    kc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
+    vc = rng.standard_normal(C * E).astype(np.float16).view(np.uint16).copy()
+    q = (2 * rng.standard_normal(E)).astype(np.float32)
     got = lvk.attention_decode(kc, vc, q, E, H, C, n_past)
     want = np.zeros(E, np.float32)
     oracle.lib.orc_attention(kc, vc, q, E, H, C, n_past, 1, want)

@@ -91,7 +91,7 @@ def sha256(path):
     return h.hexdigest()
 
 
-@pytest.mark.parametrize("name", ["tiny_q4_0", "tiny_q4_1"])
+@pytest.mark.parametrize("name", ["tiny_q4_0", "tiny_q4_1", "tiny_l80_q4_0"])
 def test_tiny_model_logits(oracle, tiny_models, name):
     g = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
     path = tiny_models[name]
