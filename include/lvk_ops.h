@@ -88,7 +88,8 @@ LVK_API void lvk_host_tables(uint16_t * exp_tab, uint16_t * silu_tab);
 
 /* decode-step profiling of a llama_context: when enabled, every eval records
  * HIP events around each kernel class (0 embed, 1 qkv, 2 attention, 3 wo,
- * 4 w1|w3, 5 w2, 6 lm_head) and accumulates device ms, launches and
+ * 4 w1|w3, 5 w2, 6 lm_head, 7 attention+wo, 8 the persistent decode kernel)
+ * and accumulates device ms, launches and
  * algorithmic weight bytes. */
 struct llama_context;
 LVK_API void lvk_set_profiling(struct llama_context * ctx, int on);
@@ -102,6 +103,12 @@ LVK_API size_t lvk_weight_bytes(struct llama_context * ctx);
 LVK_API void lvk_set_prompt_exact(struct llama_context * ctx, int on);
 /* 1 = replay the captured decode graph for single-token evals (default), 0 = eager */
 LVK_API void lvk_set_graph(struct llama_context * ctx, int on);
+/* single-token decode path: 1 = the persistent one-launch-per-token kernel
+ * (decode_persistent.hip, where the model shape is compiled in), 0 = one launch per
+ * phase (the default; env LVK_DECODE_PERSISTENT=1 makes 1 the default) */
+LVK_API void lvk_set_decode_persistent(struct llama_context * ctx, int on);
+/* 1 when the next single-token eval of ctx runs the persistent kernel */
+LVK_API int lvk_decode_persistent_active(struct llama_context * ctx);
 
 /* On-device greedy sampling.  lvk_eval_greedy(ctx, token, n_past)
  * is llama_eval(ctx, &token, 1, n_past, .) followed by

@@ -199,6 +199,60 @@ hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 
 // operator-level helpers used by the C ABI tests
 hipError_t launch_quantize_act(const float * x, int N, int K, int qtype, ActQ out, hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// Persistent single-token decode (decode_persistent.hip): the whole forward pass of
+// one token as ONE launch of one workgroup per CU, the weight stream running ahead of
+// every dependency through an LDS ring.  Q4_0 layer matrices only.
+struct DecodeLayer {            // device-resident table, one entry per layer
+    const uint4 * nib[4];       // octet images: 0 Wq|Wk|Wv, 1 Wo, 2 W1|W3, 3 W2
+    const float4 * scl[4];
+    const float * attn_norm;
+    const float * ffn_norm;
+    uint16_t * kc;              // this layer's K cache [n_ctx][E]
+    uint16_t * vc;              // and V cache [E][n_ctx]
+};
+struct DecodeArgs {
+    const DecodeLayer * layers;
+    int n_layer, n_embd, n_ff, n_head, n_ctx, n_vocab;
+    const uint4 * out_nib;      // lm_head image (nullptr: not the last pipeline stage)
+    const float4 * out_scl;
+    const float * out_norm;
+    const void * tok_emb;       // token embeddings, file layout (xin == nullptr)
+    int emb_type;
+    const float * xin;          // stage input x [E] (nullptr: the token's embedding row)
+    float * xout;               // stage output x [E] (may be nullptr)
+    const StepParams * sp;      // n_past, token (pad0)
+    float * logits;             // [V]
+    // exchange buffers (device), one slice per layer (X: two): the published residual
+    // stream [2L][E], silu(w1 x) * w3 x [L][F], this token's q | k | v rows f16 [L][3E],
+    // the quantized attention output [L][E/32]
+    float * X;
+    float * U;
+    uint16_t * cur;
+    float * aq_d;
+    uint4 * aq_qs;
+    const uint16_t * exp_tab;
+    int exp_mode;
+    const uint16_t * silu_tab;
+    const float2 * rope;        // [n_ctx][64] {cos, sin}
+    unsigned * err;             // host-mapped error word
+    // filled by launch_decode_persistent
+    unsigned * ctr;
+    unsigned long long * gran;
+    float scale;
+    int xres_rows, act_bytes, l_act, l_att, l_ring_att, n_attn_wg;
+};
+bool decode_persistent_supported(int n_embd, int n_ff, int n_head, int n_ctx, int n_vocab, int qtype);
+// floats of the per-layer attention-output scale slices (each on its own 256-byte lines)
+size_t decode_persistent_aq_d_floats(int n_embd, int n_layer);
+// counters + score granules, zeroed by the launcher before every launch
+size_t decode_persistent_scratch_bytes(int n_head, int n_ctx);
+// fill the layout fields and the scratch pointers; false when the shape is not compiled in
+bool decode_persistent_prepare(DecodeArgs & A, void * scratch, int n_cu);
+// memset of the scratch + n_cu workgroups (one per CU, all resident: the kernel's LDS
+// admits one per CU) reading the prepared arguments from A_dev (a device copy of A)
+hipError_t launch_decode_persistent(const DecodeArgs & A, const DecodeArgs * A_dev, int n_cu, hipStream_t s);
+
 }  // namespace lvk
 
 namespace lvk {

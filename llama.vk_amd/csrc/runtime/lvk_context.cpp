@@ -108,6 +108,36 @@ void Context::init(const llama_context_params & p) {
         fuse_attn_wo = getenv("LVK_FUSE_ATTN_WO") && atoi(getenv("LVK_FUSE_ATTN_WO")) != 0;
         attn_gran = model.alloc(attention_decode_scratch_bytes((int) H, (int) C));
     }
+    {
+        // persistent decode state: the layer table and the in-launch exchange buffers
+        hipDeviceProp_t prop;
+        int dev_ = 0;
+        LVK_HIP(hipGetDevice(&dev_));
+        LVK_HIP(hipGetDeviceProperties(&prop, dev_));
+        n_cu = prop.multiProcessorCount;
+        std::vector<DecodeLayer> tl(L);
+        for (size_t il = 0; il < L; ++il) {
+            const Layer & ly = model.layers[il];
+            const QMatrix * m4[4] = {&ly.wqkv, &ly.wo, &ly.w13, &ly.w2};
+            for (int k = 0; k < 4; ++k) { tl[il].nib[k] = m4[k]->nib; tl[il].scl[k] = (const float4 *) m4[k]->scl; }
+            tl[il].attn_norm = ly.attn_norm;
+            tl[il].ffn_norm = ly.ffn_norm;
+            tl[il].kc = kc + il * C * E;
+            tl[il].vc = vc + il * C * E;
+        }
+        dlayers = (DecodeLayer *) model.alloc(std::max<size_t>(1, L) * sizeof(DecodeLayer));
+        if (L) LVK_HIP(hipMemcpy(dlayers, tl.data(), L * sizeof(DecodeLayer), hipMemcpyHostToDevice));
+        const size_t Lx = std::max<size_t>(1, L);
+        xpub = (float *) model.alloc(2 * Lx * E * 4);
+        upub = (float *) model.alloc(Lx * F * 4);
+        qkv_cur = (uint16_t *) model.alloc(Lx * 3 * E * 2);
+        aq_pub_d = (float *) model.alloc(decode_persistent_aq_d_floats((int) E, (int) Lx) * 4);
+        aq_pub_qs = (uint4 *) model.alloc(Lx * (E / 32) * 16);
+        dscratch = model.alloc(decode_persistent_scratch_bytes((int) H, (int) C));
+        // opt-in: measured slower than the launch-per-phase path on 7B
+        const char * ev = getenv("LVK_DECODE_PERSISTENT");
+        decode_persistent = ev && atoi(ev) != 0;
+    }
     logits_d = (float *) model.alloc(C * V * 4);
     emb_d = (float *) model.alloc(E * 4);
     sp_d = (StepParams *) model.alloc(sizeof(StepParams));
@@ -141,6 +171,7 @@ void Context::init(const llama_context_params & p) {
     LVK_HIP(hipMemcpy(rope, rt.data(), rt.size() * sizeof(float2), hipMemcpyHostToDevice));
 
     LVK_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    prepare_persistent();
     logits.reserve(logits_all ? C * V : V);
     if (want_embedding) embedding.resize(E);
 }
@@ -184,6 +215,43 @@ void Context::collect_profile() {
         prof.ms[ev_class[i]] += ms;
     }
     ev_used = 0;
+}
+
+bool Context::persistent_ok() const { return decode_persistent && dargs_d != nullptr; }
+
+// the persistent kernel's arguments never change for a context: built and uploaded once
+void Context::prepare_persistent() {
+    const HParams & hp = model.hp;
+    if (model.layers.empty() || model.qtype != Q4_0) return;
+    DecodeArgs A{};
+    A.layers = dlayers;
+    A.n_layer = (int) model.layers.size();
+    A.n_embd = (int) hp.n_embd; A.n_ff = (int) hp.n_ff(); A.n_head = (int) hp.n_head; A.n_ctx = n_ctx;
+    A.n_vocab = (int) hp.n_vocab;
+    if (model.has_head) { A.out_nib = model.output.nib; A.out_scl = (const float4 *) model.output.scl; A.out_norm = model.norm; }
+    A.tok_emb = model.tok_emb;
+    A.emb_type = model.emb_type;
+    A.xin = model.has_embed ? nullptr : x;
+    A.xout = x;
+    A.sp = sp_d;
+    A.logits = logits_d;
+    A.X = xpub; A.U = upub; A.cur = qkv_cur; A.aq_d = aq_pub_d; A.aq_qs = aq_pub_qs;
+    A.exp_tab = exp_tab; A.exp_mode = exp_computed; A.silu_tab = silu_tab; A.rope = rope;
+    A.err = err_d;
+    if (!decode_persistent_prepare(A, dscratch, n_cu)) return;
+    dargs = A;
+    dargs_d = (DecodeArgs *) model.alloc(sizeof(DecodeArgs));
+    LVK_HIP(hipMemcpy(dargs_d, &dargs, sizeof(DecodeArgs), hipMemcpyHostToDevice));
+}
+
+void Context::set_decode_persistent(bool on) {
+    if (on == decode_persistent) return;
+    decode_persistent = on;
+    // the captured decode graphs hold the other path
+    if (graph_exec) { (void) hipGraphExecDestroy(graph_exec); graph_exec = nullptr; }
+    if (graph) { (void) hipGraphDestroy(graph); graph = nullptr; }
+    if (graph_greedy_exec) { (void) hipGraphExecDestroy(graph_greedy_exec); graph_greedy_exec = nullptr; }
+    if (graph_greedy) { (void) hipGraphDestroy(graph_greedy); graph_greedy = nullptr; }
 }
 
 static double qbytes(const QMatrix & w) { return (double) w.M * (w.K / 32) * (w.qtype == Q4_0 ? 20 : 24); }
@@ -270,6 +338,15 @@ void Context::enqueue_forward(int n, bool last_only) {
         }
         if (want_embedding)
             LVK_HIP(launch_rmsnorm_rows(x + (size_t) (n - 1) * E, model.norm, E, 1, emb_d, stream));
+        return;
+    }
+    if (n == 1 && last_only && persistent_ok()) {
+        // the whole token in one launch (decode_persistent.hip)
+        double bytes = model.has_head ? qbytes(model.output) : 0.0;
+        for (const Layer & ly : model.layers) bytes += qbytes(ly.wqkv) + qbytes(ly.wo) + qbytes(ly.w13) + qbytes(ly.w2);
+        timed_launch(K_DECODE, bytes, [&] { return launch_decode_persistent(dargs, dargs_d, n_cu, stream); });
+        if (want_embedding && model.has_head)
+            LVK_HIP(launch_rmsnorm_rows(x, model.norm, E, 1, emb_d, stream));
         return;
     }
     // single-token FFN: W1|W3 hands silu(w1 x)*(w3 x) to W2 in f32, W2 quantizes it

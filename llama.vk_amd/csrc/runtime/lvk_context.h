@@ -13,7 +13,7 @@ struct llama_context_params;
 namespace lvk {
 
 // kernel classes timed by the profiler (events around every launch of a class)
-enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_WO, K_W13, K_W2, K_LMHEAD, K_ATTN_WO, K_NCLASS };
+enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_WO, K_W13, K_W2, K_LMHEAD, K_ATTN_WO, K_DECODE, K_NCLASS };
 
 // page-locked host storage: the per-token logits D2H copy runs as one DMA instead of
 // being staged through a driver bounce buffer
@@ -83,6 +83,24 @@ struct Context {
     float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales
     float * qkv32 = nullptr;     // [C][3E] Q|K|V rows before RoPE
     float * uf = nullptr;        // [C][F] silu(w1 x) * (w3 x)
+
+    // persistent single-token decode (decode_persistent.hip): one launch per token;
+    // opt-in (env LVK_DECODE_PERSISTENT=1 or lvk_set_decode_persistent(ctx, 1)), the
+    // launch-per-phase path is the default
+    bool decode_persistent = false;
+    int n_cu = 0;
+    DecodeLayer * dlayers = nullptr;   // device layer table
+    float * xpub = nullptr;            // [2L][E] published residual stream
+    float * upub = nullptr;            // [L][F] published silu(w1 x) * w3 x
+    uint16_t * qkv_cur = nullptr;      // [L][3E] this token's q | k | v (f16)
+    float * aq_pub_d = nullptr;        // [L][E/32] the quantized attention output
+    uint4 * aq_pub_qs = nullptr;
+    void * dscratch = nullptr;         // counters + score granules (zeroed per launch)
+    DecodeArgs dargs{};                // its launch arguments (prepare_persistent)
+    DecodeArgs * dargs_d = nullptr;    // ... and their device copy (nullptr: shape not supported)
+    bool persistent_ok() const;
+    void prepare_persistent();
+    void set_decode_persistent(bool on);
 
     // decode graph (N = 1, last-token logits)
     hipGraph_t graph = nullptr;

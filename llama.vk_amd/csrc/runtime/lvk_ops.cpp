@@ -283,6 +283,8 @@ int lvk_get_profile(struct llama_context * ctx, double * ms, long * launches, do
 }
 size_t lvk_weight_bytes(struct llama_context * ctx) { return ctx->c.model.weight_bytes; }
 void lvk_set_graph(struct llama_context * ctx, int on) { ctx->c.use_graph = on != 0; }
+void lvk_set_decode_persistent(struct llama_context * ctx, int on) { ctx->c.set_decode_persistent(on != 0); }
+int lvk_decode_persistent_active(struct llama_context * ctx) { return ctx->c.persistent_ok() ? 1 : 0; }
 
 void lvk_set_prompt_exact(struct llama_context * ctx, int on) { ctx->c.prompt_exact = on != 0; }
 

@@ -98,6 +98,8 @@ _sig("lvk_get_profile", C.c_int, [C.c_void_p, f64p, i64p, f64p, C.c_int])
 _sig("lvk_reset_profile", None, [C.c_void_p])
 _sig("lvk_weight_bytes", C.c_size_t, [C.c_void_p])
 _sig("lvk_set_graph", None, [C.c_void_p, C.c_int])
+_sig("lvk_set_decode_persistent", None, [C.c_void_p, C.c_int])
+_sig("lvk_decode_persistent_active", C.c_int, [C.c_void_p])
 _sig("lvk_set_prompt_exact", None, [C.c_void_p, C.c_int])
 _sig("lvk_eval_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_argmax", C.c_int, [f32p, C.c_int])
@@ -109,7 +111,7 @@ _sig("lvk_stage_set_x", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_layers", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)])
 
 BLOCK_BYTES = {2: 20, 3: 24}
-KCLASS = ["embed", "qkv", "attention", "wo", "w13", "w2", "lm_head", "attn_wo"]
+KCLASS = ["embed", "qkv", "attention", "wo", "w13", "w2", "lm_head", "attn_wo", "decode"]
 
 
 def _check(rc, what):
@@ -223,6 +225,13 @@ class Llama:
     def set_graph(self, on):
         lib.lvk_set_graph(self.ctx, int(on))
 
+    def set_decode_persistent(self, on):
+        """single-token evals on the persistent one-launch kernel (True, default) or one launch per phase"""
+        lib.lvk_set_decode_persistent(self.ctx, int(on))
+
+    def decode_persistent_active(self):
+        return bool(lib.lvk_decode_persistent_active(self.ctx))
+
     def set_prompt_exact(self, on):
         """prompt batches on the bit-faithful VALU path (True) or the MFMA path (False, default)"""
         lib.lvk_set_prompt_exact(self.ctx, int(on))
@@ -231,10 +240,11 @@ class Llama:
         lib.lvk_reset_profile(self.ctx)
 
     def profile(self):
-        ms = np.zeros(8, np.float64)
-        la = np.zeros(8, np.int64)
-        by = np.zeros(8, np.float64)
-        n = lib.lvk_get_profile(self.ctx, ms, la, by, 8)
+        k = len(KCLASS)
+        ms = np.zeros(k, np.float64)
+        la = np.zeros(k, np.int64)
+        by = np.zeros(k, np.float64)
+        n = min(k, lib.lvk_get_profile(self.ctx, ms, la, by, k))
         return {KCLASS[i]: {"ms": float(ms[i]), "launches": int(la[i]), "bytes": float(by[i])} for i in range(n)}
 
     def weight_bytes(self):
