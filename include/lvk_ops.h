@@ -148,6 +148,35 @@ LVK_API int lvk_stage_set_x(struct llama_context * ctx, const void * buf, int n_
 /* the stage's layer range; returns the model's n_layer */
 LVK_API int lvk_stage_layers(struct llama_context * ctx, int * layer_begin, int * layer_end);
 
+/* One stage per process over RCCL (torchrun, one rank per GPU).  Rank 0 makes the
+ * communicator id (lvk_rccl_unique_id: NCCL_UNIQUE_ID_BYTES = 128 bytes into id, n >= 128)
+ * and shares it with the other ranks; every rank then joins with its stage context
+ * (lvk_init_stage with the layers of stage `stage`, on its own GPU).  lvk_stage_step runs
+ * one llama_eval slice of the pipeline on this rank: ncclRecv of inpL from stage-1, the
+ * stage's layers, ncclSend to stage+1, all on the context's stream, prompts cut into
+ * micro-batches of `micro` tokens (0: none).  greedy != 0 (one token): the last stage's
+ * device argmax is sent to stage 0; both return it.  Otherwise 0 (the last stage leaves
+ * logits for llama_get_logits).  -1 on error. */
+LVK_API int lvk_rccl_unique_id(void * id, size_t n);
+LVK_API int lvk_stage_connect(struct llama_context * ctx, const void * id, int n_stages, int stage);
+LVK_API int lvk_stage_step(struct llama_context * ctx, const int * tokens, int n_tokens, int n_past, int greedy,
+                           int micro);
+
+/* The layer split behind llama.h, one process driving n_stages HIP
+ * devices: stage s holds layers [s*L/S, (s+1)*L/S) on devices[s].  llama_eval /
+ * lvk_eval_greedy / llama_get_logits / the KV-cache calls work on the returned context as
+ * on a single-device one.  The residual stream moves between stages with grouped
+ * ncclSend/ncclRecv (transport "rccl", the default when the devices are distinct) or a
+ * stream-ordered device copy ("copy"; also used when a device repeats, e.g. a one-GPU
+ * rehearsal); the host waits once per eval.  Prompts are cut into micro-batches of
+ * `micro` tokens (0: none) that flow through the stages back to back.
+ * llama_init_from_file does the same when the environment holds LVK_SPLIT_DEVICES=0,1,..
+ * or LVK_SPLIT=S (devices 0..S-1), with LVK_SPLIT_TRANSPORT and LVK_SPLIT_MICRO (64). */
+LVK_API struct llama_context * lvk_init_split(const char * path_model, struct llama_context_params params,
+                                              int n_stages, const int * devices, const char * transport, int micro);
+/* stages of ctx (1 without a split), whether they hand off over RCCL, the micro-batch */
+LVK_API int lvk_split_info(struct llama_context * ctx, int * n_stages, int * rccl, int * micro);
+
 #ifdef __cplusplus
 }
 #endif

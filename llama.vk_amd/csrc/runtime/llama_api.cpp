@@ -15,7 +15,7 @@
 
 #include "../../../include/llama.h"
 #include "../../../include/lvk_ops.h"
-#include "lvk_context.h"
+#include "lvk_split.h"
 
 namespace {
 
@@ -166,6 +166,11 @@ void default_progress(float progress, void * ud) {
 
 }  // namespace
 
+std::vector<lvk::Context *> llama_context::stages() {
+    if (split) return split->st;
+    return {&c};
+}
+
 extern "C" {
 
 struct llama_context_params llama_context_default_params(void) {
@@ -187,8 +192,34 @@ struct llama_context_params llama_context_default_params(void) {
 bool llama_mmap_supported(void) { return true; }
 bool llama_mlock_supported(void) { return true; }
 
+// progress of stage s of S mapped onto one 0..1 sweep
+struct StageProgress {
+    void (*fn)(float, void *);
+    void * ud;
+    int s, S;
+    static void cb(float p, void * self) {
+        const StageProgress * sp = (const StageProgress *) self;
+        sp->fn((sp->s + p) / sp->S, sp->ud);
+    }
+};
+
+// load layers [layer_begin, layer_end) of the file into c on the current HIP device
+static void load_stage(lvk::Context & c, const char * path_model, const llama_context_params & params, int layer_begin,
+                       int layer_end, void (*progress)(float, void *), void * progress_ud) {
+    if (!params.f16_kv && !params.vocab_only)
+        fprintf(stderr, "llama.vk_amd: f32 KV cache not implemented on the GPU path; using f16 KV\n");
+    hipStream_t ls = nullptr;
+    if (!params.vocab_only) LVK_HIP(hipStreamCreateWithFlags(&ls, hipStreamNonBlocking));
+    struct StreamFree { hipStream_t s; ~StreamFree() { if (s) (void) hipStreamDestroy(s); } } ls_guard{ls};
+    lvk::load_model(c.model, path_model, params.vocab_only, ls, progress, progress_ud, layer_begin, layer_end);
+    c.model.hp.n_ctx = (uint32_t) params.n_ctx;
+    if (!params.vocab_only) c.init(params);
+}
+
+// devices: one HIP device per stage (empty: no split, the current device)
 static llama_context * init_context(const char * path_model, struct llama_context_params params, int layer_begin,
-                                    int layer_end) {
+                                    int layer_end, const std::vector<int> & devices = {},
+                                    const char * transport = nullptr, int micro = 64) {
     llama_context * ctx = new llama_context;
     lvk::Context & c = ctx->c;
     c.t_start_us = lvk::now_us();
@@ -200,17 +231,42 @@ static llama_context * init_context(const char * path_model, struct llama_contex
         params.progress_callback_user_data = &cur_pct;
     }
     try {
-        if (!params.f16_kv && !params.vocab_only)
-            fprintf(stderr, "llama.vk_amd: f32 KV cache not implemented on the GPU path; using f16 KV\n");
-        hipStream_t ls = nullptr;
-        if (!params.vocab_only) LVK_HIP(hipStreamCreateWithFlags(&ls, hipStreamNonBlocking));
-        lvk::load_model(c.model, path_model, params.vocab_only, ls, params.progress_callback,
-                        params.progress_callback_user_data, layer_begin, layer_end);
-        if (ls) (void) hipStreamDestroy(ls);
-        c.model.hp.n_ctx = (uint32_t) params.n_ctx;
+        if (devices.size() < 2 || params.vocab_only) {
+            load_stage(c, path_model, params, layer_begin, layer_end, params.progress_callback,
+                       params.progress_callback_user_data);
+        } else {
+            // layer split (lvk_split.h): stages 0..S-2 owned by the Split, S-1 is c
+            const int S = (int) devices.size();
+            int n_layer = 0;
+            {
+                lvk::Model probe;
+                lvk::load_model(probe, path_model, true, nullptr, nullptr, nullptr);
+                n_layer = (int) probe.hp.n_layer;
+            }
+            if (S > n_layer) throw lvk::Error("more split stages than layers");
+            ctx->split.reset(new lvk::Split);
+            lvk::Split & sp = *ctx->split;
+            sp.devices = devices;
+            sp.micro = micro;
+            for (int s = 0; s < S; ++s) {
+                lvk::DeviceGuard g(devices[s]);
+                lvk::Context * sc = &c;
+                if (s + 1 < S) {
+                    sp.owned.emplace_back(new lvk::Context);
+                    sc = sp.owned.back().get();
+                }
+                const auto lr = lvk::stage_layers(n_layer, S, s);
+                StageProgress pr{params.progress_callback, params.progress_callback_user_data, s, S};
+                load_stage(*sc, path_model, params, lr.first, lr.second, StageProgress::cb, &pr);
+                sp.st.push_back(sc);
+            }
+            sp.connect(transport);
+            fprintf(stderr, "llama_init_from_file: layer split over %d stages (%s hand-off, prompt micro-batch %d)\n",
+                    S, sp.rccl ? "RCCL send/recv" : "device copy", sp.micro);
+        }
         if (!params.vocab_only) {
-            c.init(params);
-            fprintf(stderr, "llama_init_from_file: kv self size  = %7.2f MB\n", c.kv_bytes() / 1024.0 / 1024.0);
+            size_t kvb = ctx->split ? ctx->split->kv_bytes() : c.kv_bytes();
+            fprintf(stderr, "llama_init_from_file: kv self size  = %7.2f MB\n", kvb / 1024.0 / 1024.0);
         }
     } catch (const lvk::Error & e) {
         fprintf(stderr, "error loading model: %s\n", e.msg.c_str());
@@ -222,8 +278,50 @@ static llama_context * init_context(const char * path_model, struct llama_contex
     return ctx;
 }
 
+// LVK_SPLIT_DEVICES=0,1,... (one stage per listed HIP device, in layer order; a device may
+// repeat) or LVK_SPLIT=S (devices 0..S-1); LVK_SPLIT_TRANSPORT=rccl|copy;
+// LVK_SPLIT_MICRO=tokens per prompt micro-batch (0: none)
+static std::vector<int> env_split_devices() {
+    std::vector<int> d;
+    if (const char * e = getenv("LVK_SPLIT_DEVICES")) {
+        for (const char * q = e; *q;) {
+            char * end = nullptr;
+            const long v = strtol(q, &end, 10);
+            if (end == q) break;
+            d.push_back((int) v);
+            q = *end == ',' ? end + 1 : end;
+        }
+    } else if (const char * e2 = getenv("LVK_SPLIT")) {
+        for (int i = 0; i < atoi(e2); ++i) d.push_back(i);
+    }
+    return d;
+}
+
+static int env_split_micro() {
+    const char * e = getenv("LVK_SPLIT_MICRO");
+    return e ? std::max(0, atoi(e)) : 64;
+}
+
 struct llama_context * llama_init_from_file(const char * path_model, struct llama_context_params params) {
-    return init_context(path_model, params, 0, -1);
+    return init_context(path_model, params, 0, -1, env_split_devices(), getenv("LVK_SPLIT_TRANSPORT"),
+                        env_split_micro());
+}
+
+struct llama_context * lvk_init_split(const char * path_model, struct llama_context_params params, int n_stages,
+                                      const int * devices, const char * transport, int micro) {
+    if (n_stages < 1 || !devices || micro < 0) {
+        fprintf(stderr, "%s: bad split arguments\n", __func__);
+        return nullptr;
+    }
+    return init_context(path_model, params, 0, -1, std::vector<int>(devices, devices + n_stages), transport, micro);
+}
+
+int lvk_split_info(struct llama_context * ctx, int * n_stages, int * rccl, int * micro) {
+    const lvk::Split * sp = ctx->split.get();
+    if (n_stages) *n_stages = sp ? (int) sp->st.size() : 1;
+    if (rccl) *rccl = sp && sp->rccl ? 1 : 0;
+    if (micro) *micro = sp ? sp->micro : 0;
+    return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -266,6 +364,53 @@ int lvk_stage_layers(struct llama_context * ctx, int * layer_begin, int * layer_
     return (int) ctx->c.model.hp.n_layer;
 }
 
+int lvk_rccl_unique_id(void * id, size_t n) {
+    try {
+        if (!id || n < sizeof(ncclUniqueId)) throw lvk::Error("id buffer smaller than NCCL_UNIQUE_ID_BYTES");
+        const lvk::Rccl & R = lvk::Rccl::get();
+        ncclUniqueId u;
+        R.check(R.GetUniqueId(&u), "ncclGetUniqueId");
+        std::memcpy(id, &u, sizeof(u));
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());
+        return -1;
+    }
+    return 0;
+}
+
+int lvk_stage_connect(struct llama_context * ctx, const void * id, int n_stages, int stage) {
+    try {
+        lvk::Context & c = ctx->c;
+        if (ctx->split || n_stages < 1 || stage < 0 || stage >= n_stages || !id)
+            throw lvk::Error("bad stage link arguments");
+        if ((stage == 0) != c.model.has_embed || (stage == n_stages - 1) != c.model.has_head)
+            throw lvk::Error("the context's layer range does not match its stage position");
+        const lvk::Rccl & R = lvk::Rccl::get();
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        std::unique_ptr<lvk::StageLink, lvk::StageLinkDel> L(new lvk::StageLink);
+        L->stage = stage;
+        L->n_stages = n_stages;
+        lvk::DeviceGuard g(c.device);
+        R.check(R.CommInitRank(&L->comm, n_stages, u, stage), "ncclCommInitRank");
+        c.link = std::move(L);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());
+        return -1;
+    }
+    return 0;
+}
+
+int lvk_stage_step(struct llama_context * ctx, const llama_token * tokens, int n_tokens, int n_past, int greedy,
+                   int micro) {
+    try {
+        return lvk::stage_step(ctx->c, tokens, n_tokens, n_past, greedy != 0, micro);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());
+        return -1;
+    }
+}
+
 void llama_free(struct llama_context * ctx) { delete ctx; }
 
 int llama_eval(struct llama_context * ctx, const llama_token * tokens, int n_tokens, int n_past, int n_threads) {
@@ -273,7 +418,8 @@ int llama_eval(struct llama_context * ctx, const llama_token * tokens, int n_tok
     lvk::Context & c = ctx->c;
     const int64_t t0 = lvk::now_us();
     try {
-        c.eval(tokens, n_tokens, n_past);
+        if (ctx->split) ctx->split->eval(tokens, n_tokens, n_past);
+        else c.eval(tokens, n_tokens, n_past);
     } catch (const lvk::Error & e) {
         fprintf(stderr, "%s: failed to eval: %s\n", __func__, e.msg.c_str());
         return 1;
@@ -326,17 +472,27 @@ llama_token llama_sample_top_p_top_k(struct llama_context * ctx, const llama_tok
 }
 
 const uint8_t * llama_get_kv_cache(struct llama_context * ctx) {
-    try { ctx->c.kv_get(); } catch (const lvk::Error & e) { fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str()); }
+    try {
+        if (ctx->split) ctx->split->kv_get(ctx->c.kv_host);
+        else ctx->c.kv_get();
+    } catch (const lvk::Error & e) { fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str()); }
     return ctx->c.kv_host.data();
 }
-size_t llama_get_kv_cache_size(struct llama_context * ctx) { return ctx->c.kv_bytes(); }
+size_t llama_get_kv_cache_size(struct llama_context * ctx) {
+    return ctx->split ? ctx->split->kv_bytes() : ctx->c.kv_bytes();
+}
 int llama_get_kv_cache_token_count(struct llama_context * ctx) { return ctx->c.kv_n; }
 void llama_set_kv_cache(struct llama_context * ctx, const uint8_t * kv_cache, size_t n_size, int n_token_count) {
-    if (n_size != ctx->c.kv_bytes()) {   // LLAMA_ASSERT in the reference (llama.cpp:1696)
+    if (n_size != llama_get_kv_cache_size(ctx)) {   // LLAMA_ASSERT in the reference (llama.cpp:1696)
         fprintf(stderr, "llama_set_kv_cache: size mismatch\n");
         abort();
     }
-    ctx->c.kv_set(kv_cache, n_size);
+    try {
+        if (ctx->split) ctx->split->kv_set(kv_cache, n_size);
+        else ctx->c.kv_set(kv_cache, n_size);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());
+    }
     ctx->c.kv_n = n_token_count;
 }
 

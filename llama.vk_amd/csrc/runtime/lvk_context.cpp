@@ -142,7 +142,7 @@ void Context::init(const llama_context_params & p) {
     emb_d = (float *) model.alloc(E * 4);
     sp_d = (StepParams *) model.alloc(sizeof(StepParams));
     tok_d = (int *) model.alloc(C * 4);
-    LVK_HIP(hipHostMalloc((void **) &sp_h, sizeof(StepParams), hipHostMallocDefault));
+    LVK_HIP(hipHostMalloc((void **) &sp_h, (1 + C) * sizeof(StepParams), hipHostMallocDefault));
     LVK_HIP(hipHostMalloc((void **) &tok_h, C * 4, hipHostMallocDefault));
     LVK_HIP(hipGetDevice(&device));
     LVK_HIP(hipHostMalloc((void **) &err_h, 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -277,8 +277,10 @@ bool Context::use_mfma(int n) const {
     return true;
 }
 
-void Context::enqueue_forward(int n, bool last_only) {
+void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int logit_row, bool head) {
     const HParams & hp = model.hp;
+    if (!tok_src) tok_src = tok_d;
+    float * const logits_out = logits_d + (size_t) logit_row * hp.n_vocab;
     const int E = (int) hp.n_embd, H = (int) hp.n_head, hd = E / H, F = (int) hp.n_ff();
     const size_t CE = (size_t) n_ctx * E;
     if (use_mfma(n)) {
@@ -286,7 +288,7 @@ void Context::enqueue_forward(int n, bool last_only) {
         //   act(norm) -> QKV (store) -> RoPE + KV append -> attention -> act -> Wo (+x)
         //   act(norm) -> W1|W3 (silu * mul) -> act -> W2 (+x)
         if (model.has_embed)
-            timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_d, n, x, stream); });
+            timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_src, n, x, stream); });
         for (size_t il = 0; il < model.layers.size(); ++il) {
             const Layer & ly = model.layers[il];
             uint16_t * kcl = kc + il * CE;
@@ -322,17 +324,17 @@ void Context::enqueue_forward(int n, bool last_only) {
                 return launch_mm_mfma(ly.w2, xh, xda, n, x, E, 0, EPI_RESID, nullptr, stream);
             });
         }
-        if (!model.has_head) return;
+        if (!model.has_head || !head) return;
         if (last_only || !mm_mfma_supported(model.output)) {
             MvLaunch o;
-            o.w = model.output; o.x = x; o.g = model.norm; o.sp = sp_d; o.y = logits_d;
+            o.w = model.output; o.x = x; o.g = model.norm; o.sp = sp_d; o.y = logits_out;
             o.tok0 = last_only ? n - 1 : 0;
             o.n_tokens = last_only ? 1 : n;
             timed_launch(K_LMHEAD, qbytes(model.output), [&] { return mv_launch(o, PRO_NORM, EPI_STORE, stream); });
         } else {
             timed_launch(K_LMHEAD, 0, [&] { return launch_act_f16(x, model.norm, n, E, xh, xda, stream); });
             timed_launch(K_LMHEAD, qbytes(model.output), [&] {
-                return launch_mm_mfma(model.output, xh, xda, n, logits_d, (int) hp.n_vocab, 0, EPI_STORE, nullptr,
+                return launch_mm_mfma(model.output, xh, xda, n, logits_out, (int) hp.n_vocab, 0, EPI_STORE, nullptr,
                                       stream);
             });
         }
@@ -340,7 +342,7 @@ void Context::enqueue_forward(int n, bool last_only) {
             LVK_HIP(launch_rmsnorm_rows(x + (size_t) (n - 1) * E, model.norm, E, 1, emb_d, stream));
         return;
     }
-    if (n == 1 && last_only && persistent_ok()) {
+    if (n == 1 && last_only && head && persistent_ok()) {
         // the whole token in one launch (decode_persistent.hip)
         double bytes = model.has_head ? qbytes(model.output) : 0.0;
         for (const Layer & ly : model.layers) bytes += qbytes(ly.wqkv) + qbytes(ly.wo) + qbytes(ly.w13) + qbytes(ly.w2);
@@ -360,7 +362,7 @@ void Context::enqueue_forward(int n, bool last_only) {
     if (model.has_embed)
         // a single-token eval takes its token from the step block (one H2D copy per token)
         timed_launch(K_EMBED, 0, [&] {
-            return launch_embed(model.tok_emb, model.emb_type, E, n == 1 ? &sp_d->pad0 : tok_d, n, x, stream);
+            return launch_embed(model.tok_emb, model.emb_type, E, n == 1 ? &sp_d->pad0 : tok_src, n, x, stream);
         });
     for (size_t il = 0; il < model.layers.size(); ++il) {
         const Layer & ly = model.layers[il];
@@ -402,9 +404,9 @@ void Context::enqueue_forward(int n, bool last_only) {
             timed_launch(K_W2, qbytes(ly.w2), [&] { return launch_matvec(d, PRO_ACTQ, EPI_RESID, stream); });
         }
     }
-    if (!model.has_head) return;   // not the last pipeline stage: x is the output
+    if (!model.has_head || !head) return;   // not the last pipeline stage: x is the output
     MvLaunch o;
-    o.w = model.output; o.x = x; o.g = model.norm; o.sp = sp_d; o.y = logits_d;
+    o.w = model.output; o.x = x; o.g = model.norm; o.sp = sp_d; o.y = logits_out;
     o.tok0 = last_only ? n - 1 : 0;
     o.n_tokens = last_only ? 1 : n;
     timed_launch(K_LMHEAD, qbytes(model.output), [&] { return mv_launch(o, PRO_NORM, EPI_STORE, stream); });
@@ -443,65 +445,76 @@ void Context::build_graph(bool greedy) {
 // of llama_sample_top_p_top_k(temp <= 0) (llama.cpp:1382-1394) over the logits in
 // HBM.  Host logits are not refreshed (llama_get_logits keeps the previous eval's).
 int Context::eval_greedy(int token, int n_past) {
-    const int V = (int) model.hp.n_vocab;
     if (!model.has_head || !model.has_embed) throw Error("llama.vk_amd: greedy eval needs the whole model");
-    if (n_past < 0 || n_past + 1 > n_ctx) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
-    if (token < 0 || token >= V) throw Error("llama.vk_amd: token id out of range");
-    tok_h[0] = token;
-    sp_h->n_past = n_past;
-    sp_h->n_tokens = 1;
-    sp_h->pad0 = token;
-    if (use_graph && !profiling) {
-        if (!graph_greedy_exec) build_graph(true);
-        LVK_HIP(hipGraphLaunch(graph_greedy_exec, stream));
-    } else {
-        LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
-        enqueue_forward(1, true);
-        LVK_HIP(launch_argmax(logits_d, V, greedy_d, stream));
-        LVK_HIP(hipMemcpyAsync(greedy_h, greedy_d, sizeof(int), hipMemcpyDeviceToHost, stream));
-    }
-    LVK_HIP(hipStreamSynchronize(stream));
-    if (profiling) collect_profile();
-    check_device_error();
-    logits_valid = false;     // llama_get_logits still holds an earlier eval's row
+    EvalPart part;
+    part.greedy = true;
+    begin_eval(&token, 1, n_past, part);
+    end_eval(true);
     return *greedy_h;
 }
 
 void Context::eval(const int * tokens, int n, int n_past) {
+    begin_eval(tokens, n, n_past, EvalPart{});
+    end_eval(false);
+}
+
+void Context::begin_eval(const int * tokens, int n, int n_past, const EvalPart & part) {
     const HParams & hp = model.hp;
     const int V = (int) hp.n_vocab;
-    if (n <= 0 || n_past < 0 || n_past + n > n_ctx) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
+    const int n_total = part.n_total < 0 ? n : part.n_total;
+    if (n <= 0 || n_past < 0 || n_past + n > n_ctx || part.tok_off < 0 || part.tok_off + n > n_total)
+        throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
+    if (part.greedy && (!model.has_head || n != 1 || logits_all))
+        throw Error("llama.vk_amd: greedy eval needs the lm_head stage, one token and last-token logits");
     if (model.has_embed) {
         if (!tokens) throw Error("llama.vk_amd: the first stage needs tokens");
         for (int i = 0; i < n; ++i)
             if (tokens[i] < 0 || tokens[i] >= V) throw Error("llama.vk_amd: token id out of range");
-        std::memcpy(tok_h, tokens, sizeof(int) * (size_t) n);
+        std::memcpy(tok_h + part.tok_off, tokens, sizeof(int) * (size_t) n);
     }
-    sp_h->n_past = n_past;
-    sp_h->n_tokens = n;
-    sp_h->pad0 = (n == 1 && model.has_embed) ? tokens[0] : 0;
     const bool last_only = !logits_all;
-    const int rows = last_only ? 1 : n;
-    if (model.has_head) logits.resize((size_t) rows * V);   // within the reserve: the pointer never moves
-    if (n == 1 && last_only && use_graph && !profiling) {
-        if (!graph_exec) build_graph();
-        LVK_HIP(hipGraphLaunch(graph_exec, stream));
+    const bool single = part.n_total < 0 || part.n_total == n;
+    const bool graph_ok = n == 1 && last_only && single && use_graph && !profiling;
+    // the graphs read step block 0; eager slices each take their own (the H2D copy reads
+    // the pinned block when it executes, after the host may have queued further slices)
+    if (!graph_ok && sp_next > n_ctx) throw Error("llama.vk_amd: too many slices before a sync");
+    StepParams * sh = graph_ok ? sp_h : sp_h + sp_next++;
+    sh->n_past = n_past;
+    sh->n_tokens = n;
+    sh->pad0 = (n == 1 && model.has_embed) ? tokens[0] : 0;
+    if (model.has_head && part.tok_off == 0)   // within the reserve: the pointer never moves
+        logits.resize((size_t) (last_only ? 1 : n_total) * V);
+    if (graph_ok) {
+        hipGraphExec_t & ge = part.greedy ? graph_greedy_exec : graph_exec;
+        if (!ge) build_graph(part.greedy);
+        LVK_HIP(hipGraphLaunch(ge, stream));
     } else {
-        LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
-        if (n > 1) LVK_HIP(hipMemcpyAsync(tok_d, tok_h, sizeof(int) * (size_t) n, hipMemcpyHostToDevice, stream));
-        enqueue_forward(n, last_only);
-        if (model.has_head)
+        LVK_HIP(hipMemcpyAsync(sp_d, sh, sizeof(StepParams), hipMemcpyHostToDevice, stream));
+        if (n > 1)
+            LVK_HIP(hipMemcpyAsync(tok_d + part.tok_off, tok_h + part.tok_off, sizeof(int) * (size_t) n,
+                                   hipMemcpyHostToDevice, stream));
+        enqueue_forward(n, last_only, tok_d + part.tok_off, last_only ? 0 : part.tok_off, part.head);
+        if (part.greedy) {
+            LVK_HIP(launch_argmax(logits_d, V, greedy_d, stream));
+            LVK_HIP(hipMemcpyAsync(greedy_h, greedy_d, sizeof(int), hipMemcpyDeviceToHost, stream));
+        } else if (model.has_head && part.copy_out) {
             LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost,
                                    stream));
+        }
     }
-    if (want_embedding && model.has_head) {
+    if (want_embedding && model.has_head && part.copy_out && !part.greedy) {
         embedding.resize(hp.n_embd);
         LVK_HIP(hipMemcpyAsync(embedding.data(), emb_d, sizeof(float) * hp.n_embd, hipMemcpyDeviceToHost, stream));
     }
+}
+
+void Context::end_eval(bool greedy) {
+    sp_next = 1;
     LVK_HIP(hipStreamSynchronize(stream));
     if (profiling) collect_profile();
     check_device_error();
-    logits_valid = model.has_head;
+    // after lvk_eval_greedy llama_get_logits still holds an earlier eval's row
+    logits_valid = model.has_head && !greedy;
 }
 
 size_t Context::kv_bytes() const {

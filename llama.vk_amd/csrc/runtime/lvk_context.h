@@ -6,11 +6,17 @@
 #include <array>
 #include <chrono>
 #include <functional>
+#include <memory>
 #include <new>
 
 struct llama_context_params;
 
 namespace lvk {
+
+struct Split;       // lvk_split.h
+struct StageLink;
+struct SplitDel { void operator()(Split * p) const; };
+struct StageLinkDel { void operator()(StageLink * p) const; };
 
 // kernel classes timed by the profiler (events around every launch of a class)
 enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_WO, K_W13, K_W2, K_LMHEAD, K_ATTN_WO, K_DECODE, K_NCLASS };
@@ -41,6 +47,16 @@ struct Profile {
     std::array<double, K_NCLASS> bytes{};    // algorithmic HBM bytes accumulated
 };
 
+// one slice of an eval call: a whole llama_eval, or one micro-batch of a prompt that a
+// layer split pipelines through its stages (lvk_split.cpp)
+struct EvalPart {
+    int tok_off = 0;      // first token of this slice within the call
+    int n_total = -1;     // tokens of the whole call (-1: this slice is the call)
+    bool head = true;     // run norm + lm_head (last stage: the call's last slice, or logits_all)
+    bool copy_out = true; // copy logits / embedding / the greedy token to the host after this slice
+    bool greedy = false;  // end in the device argmax (lvk_eval_greedy) instead of the logits D2H
+};
+
 struct Context {
     Model model;
     int n_ctx = 512;
@@ -65,11 +81,13 @@ struct Context {
     float2 * rope = nullptr;     // [n_ctx][hd/2]
     StepParams * sp_d = nullptr;
     int * tok_d = nullptr;       // [n_ctx]
-    StepParams * sp_h = nullptr; // pinned
-    int * tok_h = nullptr;       // pinned
+    StepParams * sp_h = nullptr; // pinned, [1 + n_ctx] step blocks: [0] for the graphs, the
+    int sp_next = 1;             //   rest one per eager slice enqueued before the next sync
+    int * tok_h = nullptr;       // pinned [n_ctx]
     unsigned * err_h = nullptr;  // pinned, mapped: the kernels' error word (lvk_kernels.h DevError)
     unsigned * err_d = nullptr;  // its device address
     int device = 0;              // the HIP device of this context
+    std::unique_ptr<StageLink, StageLinkDel> link;   // one-stage-per-process RCCL link (lvk_stage_connect)
 
     // prompt (N > 1) path: MFMA matmuls with exact block dots (default) or the
     // bit-faithful VALU kernels (prompt_exact; env LVK_PROMPT_EXACT=1)
@@ -135,9 +153,14 @@ struct Context {
     ~Context();
     void init(const llama_context_params & p);
     void eval(const int * tokens, int n, int n_past);
+    // eval = begin_eval (everything enqueued on `stream`, no host wait) + end_eval (sync,
+    // profile, device error word); a layer split interleaves the stages' begin_evals
+    // with the residual-stream hand-offs and ends them together
+    void begin_eval(const int * tokens, int n, int n_past, const EvalPart & part);
+    void end_eval(bool greedy);
     // stage boundary: copy the residual stream x [n][E] to (to_ctx) or from the context
     void x_copy(void * buf, int n, bool to_ctx, bool on_device);
-    void enqueue_forward(int n, bool last_only);
+    void enqueue_forward(int n, bool last_only, const int * tok_src = nullptr, int logit_row = 0, bool head = true);
     bool use_mfma(int n) const;
     void build_graph(bool greedy = false);
     int eval_greedy(int token, int n_past);
@@ -161,5 +184,8 @@ void host_fp16_tables(std::vector<uint16_t> & exp_tab, std::vector<uint16_t> & s
 
 // the opaque handle of the C API (include/llama.h)
 struct llama_context {
-    lvk::Context c;
+    lvk::Context c;                                  // the whole model, or the last stage of a split
+    std::unique_ptr<lvk::Split, lvk::SplitDel> split;   // layer split over devices (lvk_split.h)
+    // every stage context in layer order (just &c without a split)
+    std::vector<lvk::Context *> stages();
 };

@@ -8,7 +8,7 @@
 
 #include "../../../include/llama.h"
 #include "../../../include/lvk_ops.h"
-#include "lvk_context.h"
+#include "lvk_split.h"
 
 namespace {
 
@@ -271,26 +271,51 @@ void lvk_host_tables(uint16_t * exp_tab, uint16_t * silu_tab) {
     std::memcpy(silu_tab, ts.data(), 65536 * 2);
 }
 
-void lvk_set_profiling(struct llama_context * ctx, int on) { ctx->c.profiling = on != 0; }
-void lvk_reset_profile(struct llama_context * ctx) { ctx->c.prof = lvk::Profile{}; }
+// settings and profiles of a layer-split context cover every stage
+void lvk_set_profiling(struct llama_context * ctx, int on) {
+    for (lvk::Context * c : ctx->stages()) c->profiling = on != 0;
+}
+void lvk_reset_profile(struct llama_context * ctx) {
+    for (lvk::Context * c : ctx->stages()) c->prof = lvk::Profile{};
+}
 int lvk_get_profile(struct llama_context * ctx, double * ms, long * launches, double * bytes, int n) {
     for (int i = 0; i < n && i < lvk::K_NCLASS; ++i) {
-        ms[i] = ctx->c.prof.ms[i];
-        launches[i] = ctx->c.prof.launches[i];
-        bytes[i] = ctx->c.prof.bytes[i];
+        ms[i] = 0;
+        launches[i] = 0;
+        bytes[i] = 0;
+        for (lvk::Context * c : ctx->stages()) {
+            ms[i] += c->prof.ms[i];
+            launches[i] += c->prof.launches[i];
+            bytes[i] += c->prof.bytes[i];
+        }
     }
     return lvk::K_NCLASS;
 }
-size_t lvk_weight_bytes(struct llama_context * ctx) { return ctx->c.model.weight_bytes; }
-void lvk_set_graph(struct llama_context * ctx, int on) { ctx->c.use_graph = on != 0; }
-void lvk_set_decode_persistent(struct llama_context * ctx, int on) { ctx->c.set_decode_persistent(on != 0); }
-int lvk_decode_persistent_active(struct llama_context * ctx) { return ctx->c.persistent_ok() ? 1 : 0; }
+size_t lvk_weight_bytes(struct llama_context * ctx) {
+    size_t b = 0;
+    for (lvk::Context * c : ctx->stages()) b += c->model.weight_bytes;
+    return b;
+}
+void lvk_set_graph(struct llama_context * ctx, int on) {
+    for (lvk::Context * c : ctx->stages()) c->use_graph = on != 0;
+}
+void lvk_set_decode_persistent(struct llama_context * ctx, int on) {
+    for (lvk::Context * c : ctx->stages()) c->set_decode_persistent(on != 0);
+}
+int lvk_decode_persistent_active(struct llama_context * ctx) {
+    for (lvk::Context * c : ctx->stages())
+        if (!c->persistent_ok()) return 0;
+    return 1;
+}
 
-void lvk_set_prompt_exact(struct llama_context * ctx, int on) { ctx->c.prompt_exact = on != 0; }
+void lvk_set_prompt_exact(struct llama_context * ctx, int on) {
+    for (lvk::Context * c : ctx->stages()) c->prompt_exact = on != 0;
+}
 
 int lvk_kv_copy(struct llama_context * dst, struct llama_context * src, int n_tokens) {
     try {
         if (!dst || !src || dst == src) throw lvk::Error("need two distinct contexts");
+        if (dst->split || src->split) throw lvk::Error("layer-split contexts copy KV state through llama_get_kv_cache");
         dst->c.kv_copy_from(src->c, n_tokens);
         return 0;
     } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
@@ -314,7 +339,12 @@ int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past) {
     const int64_t t0 = lvk::now_us();
     int r;
     try {
-        r = c.eval_greedy(token, n_past);
+        if (ctx->split) {
+            ctx->split->eval(&token, 1, n_past, true);
+            r = *c.greedy_h;
+        } else {
+            r = c.eval_greedy(token, n_past);
+        }
     } catch (const lvk::Error & e) {
         fprintf(stderr, "%s: failed to eval: %s\n", __func__, e.msg.c_str());
         return -1;

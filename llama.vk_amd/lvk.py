@@ -109,6 +109,11 @@ _sig("lvk_stage_eval", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_get_x", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_set_x", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_layers", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)])
+_sig("lvk_rccl_unique_id", C.c_int, [C.c_void_p, C.c_size_t])
+_sig("lvk_stage_connect", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
+_sig("lvk_stage_step", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int])
+_sig("lvk_init_split", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, i32p, C.c_char_p, C.c_int])
+_sig("lvk_split_info", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)])
 
 BLOCK_BYTES = {2: 20, 3: 24}
 KCLASS = ["embed", "qkv", "attention", "wo", "w13", "w2", "lm_head", "attn_wo", "decode"]
@@ -123,8 +128,10 @@ class Llama:
     """One llama_context (reference llama.h API, GPU forward pass)."""
 
     def __init__(self, path, n_ctx=512, seed=1, logits_all=False, embedding=False, vocab_only=False, f16_kv=True,
-                 layers=None):
-        """layers=(begin, end): a pipeline stage holding only those layers (lvk_init_stage)"""
+                 layers=None, split=None, transport=None, micro=64):
+        """layers=(begin, end): a pipeline stage holding only those layers (lvk_init_stage);
+        split=[dev0, dev1, ...]: the whole model layer-split over those HIP devices in this
+        process (lvk_init_split; transport "rccl" / "copy" / None = rccl when distinct)"""
         p = lib.llama_context_default_params()
         p.n_ctx = n_ctx
         p.seed = seed
@@ -134,7 +141,11 @@ class Llama:
         p.vocab_only = vocab_only
         self._cb = PROGRESS_CB(lambda prog, ud: None)
         p.progress_callback = self._cb
-        if layers is None:
+        if split is not None:
+            d = np.ascontiguousarray(split, np.int32)
+            self.ctx = lib.lvk_init_split(path.encode(), p, len(d), d, transport.encode() if transport else None,
+                                          int(micro))
+        elif layers is None:
             self.ctx = lib.llama_init_from_file(path.encode(), p)
         else:
             self.ctx = lib.lvk_init_stage(path.encode(), p, int(layers[0]), int(layers[1]))
@@ -184,6 +195,28 @@ class Llama:
     def set_x(self, ptr, n_tokens, on_device):
         _check(lib.lvk_stage_set_x(self.ctx, C.c_void_p(ptr), n_tokens, int(on_device)), "lvk_stage_set_x")
 
+    def split_info(self):
+        """(stages, rccl, micro) of a layer-split context; (1, False, 0) otherwise"""
+        a, b, c = C.c_int(), C.c_int(), C.c_int()
+        lib.lvk_split_info(self.ctx, C.byref(a), C.byref(b), C.byref(c))
+        return a.value, bool(b.value), c.value
+
+    def stage_connect(self, uid, n_stages, stage):
+        """join the RCCL communicator of a one-stage-per-process pipeline (lvk_stage_connect)"""
+        buf = C.create_string_buffer(bytes(uid), 128)
+        _check(lib.lvk_stage_connect(self.ctx, buf, int(n_stages), int(stage)), "lvk_stage_connect")
+
+    def stage_step(self, tokens, n_tokens, n_past, greedy=False, micro=64):
+        """recv inpL -> this stage's layers -> send (lvk_stage_step); the greedy token on the
+        first/last stage when greedy"""
+        t = None if tokens is None else np.ascontiguousarray(tokens, np.int32)
+        r = lib.lvk_stage_step(self.ctx, None if t is None else t.ctypes.data, int(n_tokens), int(n_past),
+                               int(greedy), int(micro))
+        if r < 0:
+            raise RuntimeError("lvk_stage_step failed")
+        self._last_n = n_tokens
+        return r
+
     def stage_layers(self):
         b, e = C.c_int(), C.c_int()
         n = lib.lvk_stage_layers(self.ctx, C.byref(b), C.byref(e))
@@ -226,7 +259,7 @@ class Llama:
         lib.lvk_set_graph(self.ctx, int(on))
 
     def set_decode_persistent(self, on):
-        """single-token evals on the persistent one-launch kernel (True, default) or one launch per phase"""
+        """single-token evals on the persistent one-launch kernel (True) or one launch per phase (False, default)"""
         lib.lvk_set_decode_persistent(self.ctx, int(on))
 
     def decode_persistent_active(self):
@@ -393,3 +426,10 @@ def gen_model(path, n_embd=4096, n_head=32, n_layer=32, ftype=2, seed=1, n_vocab
         cmd += ["--vocab", vocab]
     subprocess.check_call(cmd, stderr=subprocess.DEVNULL)
     return path
+
+
+def rccl_unique_id():
+    """a fresh RCCL communicator id (128 bytes) for lvk_stage_connect; rank 0 makes it"""
+    buf = C.create_string_buffer(128)
+    _check(lib.lvk_rccl_unique_id(buf, 128), "lvk_rccl_unique_id")
+    return buf.raw

@@ -70,6 +70,40 @@ def test_dropin_main_greedy_text_matches_reference_cpu(tiny_models):
     assert b"llama_print_timings" in gpu_err
 
 
+@pytest.mark.gpu
+def test_dropin_main_context_swap_matches_reference_cpu(tiny_models):
+    """main's infinite generation (main.cpp:246-266): at n_ctx 64 with --keep 4 it keeps
+    the first 4 prompt tokens and re-evaluates half of the last 60 as one batch, over and
+    over; the GPU library and the reference CPU build print the same text"""
+    exe = os.path.join(DROPIN, "main")
+    _need(exe)
+    _need(REF_MAIN)
+    args = ["-m", tiny_models["tiny_q4_0"], "-p", "Building a website can be done in 10 simple steps:",
+            "-n", "160", "--temp", "0", "-s", "1", "-c", "64", "--keep", "4", "--ignore-eos"]
+    gpu_out, _ = _run([exe] + args + ["-t", "1"])
+    cpu_out, _ = _run([REF_MAIN] + args + ["-t", "8"])
+    assert gpu_out == cpu_out
+    assert len(gpu_out) > 200
+
+
+@pytest.mark.gpu
+def test_dropin_main_layer_split_matches_reference_cpu(tiny_models):
+    """the unmodified main on a 3-stage layer split (LVK_SPLIT_DEVICES; one GPU here, so the
+    stages hand off by device copy) with 8-token prompt micro-batches: the same text"""
+    exe = os.path.join(DROPIN, "main")
+    _need(exe)
+    _need(REF_MAIN)
+    args = ["-m", tiny_models["tiny_q4_0"], "-p", "Building a website can be done in 10 simple steps:",
+            "-n", "48", "--temp", "0", "-s", "1", "-c", "256", "--ignore-eos"]
+    env = dict(os.environ, LVK_SPLIT_DEVICES="0,0,0", LVK_SPLIT_MICRO="8")
+    p = subprocess.run([exe] + args + ["-t", "1"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300,
+                       env=env)
+    assert p.returncode == 0, p.stderr.decode(errors="replace")[-2000:]
+    assert b"layer split over 3 stages" in p.stderr
+    cpu_out, _ = _run([REF_MAIN] + args + ["-t", "8"])
+    assert p.stdout == cpu_out
+
+
 def _ppl_values(out):
     """the `[i]ppl,` fields examples/perplexity prints (perplexity.cpp:76)"""
     import re
