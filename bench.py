@@ -170,50 +170,101 @@ def cpu_baseline(path, budget_s=20.0):
             "host": info}
 
 
-def layer_split_decode(args, m_full, rank, ws, local, pg, n_ctx, ptoks):
-    """greedy decode through a ws-stage layer split of the 7B file (one stage per
-    rank, residual stream over RCCL send/recv); returns the rank-0 report"""
-    import datetime
+SPLIT_TIMEOUT_S = 420
+
+
+def split_child(args):
+    """one pipeline stage in a child process (bench.py --split-child): the C++ stage link
+    (lvk_stage_connect / lvk_stage_step: ncclRecv -> this stage's layers -> ncclSend on the
+    stage's stream, greedy token relayed from the last stage to the first).  Prints one
+    JSON line."""
     import numpy as np
-    import torch
-    import torch.distributed as dist
     import lvk
-    from pipeline import StagePipeline, layer_ranges
-    on_device = args.split_backend == "nccl"
-    dev = local % torch.cuda.device_count()
-    torch.cuda.set_device(dev)
-    with _StdoutToStderr():
-        grp = dist.new_group(backend=args.split_backend, timeout=datetime.timedelta(seconds=120))
-    path = args.split_model or args.model
-    hp = lvk.model_hparams(path)
-    lr = layer_ranges(hp["n_layer"], ws)[rank]
-    st = lvk.Llama(path, n_ctx=n_ctx, layers=lr)
-    pipe = StagePipeline(st, hp["n_embd"], n_ctx, dist, on_device=on_device, device="cuda:%d" % dev, group=grp)
-    lg = pipe.eval(list(ptoks), 0)
-    tok = pipe.greedy_next(lg)
-    n_past = len(ptoks)
-    for _ in range(4):
-        lg = pipe.eval([tok], n_past)
-        tok = pipe.greedy_next(lg)
+    S, s = args.split_stages, args.split_stage
+    lvk.set_device(args.split_device)
+    hp = lvk.model_hparams(args.split_model)
+    L = hp["n_layer"]
+    lr = (s * L // S, (s + 1) * L // S)
+    t0 = time.time()
+    st = lvk.Llama(args.split_model, n_ctx=512, layers=lr)
+    load_s = time.time() - t0
+    st.stage_connect(bytes.fromhex(args.split_uid), S, s)
+    ptoks = np.array(prompt_tokens(16), np.int32)
+    first = s == 0
+    st.stage_step(ptoks if first else None, 16, 0, micro=args.split_micro)
+    tok, n_past = 1000, 16
+    for _ in range(args.warmup):
+        tok = st.stage_step(np.array([tok], np.int32) if first else None, 1, n_past, greedy=True)
         n_past += 1
-    dist.barrier(group=grp)
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps_split):
-        lg = pipe.eval([tok], n_past)
-        tok = pipe.greedy_next(lg)
-        n_past = n_past + 1 if n_past + 1 < n_ctx else len(ptoks)
-    torch.cuda.synchronize()
-    dist.barrier(group=grp)
-    dt = all_max(pg, time.perf_counter() - t0)
+    for _ in range(args.steps_split):
+        tok = st.stage_step(np.array([tok], np.int32) if first else None, 1, n_past, greedy=True)
+        n_past = n_past + 1 if n_past + 1 < 512 else 16
+    dec = time.perf_counter() - t0
+    # a 512-token prompt through the pipeline, with and without micro-batches (every rank
+    # times its own stage_step; the last stage's time is the pipeline's)
+    p512 = np.array(prompt_tokens(512), np.int32)
+    pre = {}
+    for micro in (args.split_micro, 0):
+        best = 1e30
+        for _ in range(2):
+            st.stage_step(np.array([tok], np.int32) if first else None, 1, 16, greedy=True)   # re-sync the stages
+            t0 = time.perf_counter()
+            st.stage_step(p512 if first else None, 512, 0, micro=micro)
+            best = min(best, time.perf_counter() - t0)
+        pre[micro] = best
     st.close()
-    return {"value": args.steps_split / dt, "unit": "tok/s", "stages": ws, "steps": args.steps_split,
-            "layers_per_stage": [list(x) for x in layer_ranges(hp["n_layer"], ws)],
-            "workload": "%s greedy decode, layers split over %d ranks (one stage per rank), residual "
-                        "stream f32 [n_embd] per token over %s send/recv"
-                        % (os.path.basename(path), ws, "RCCL" if on_device else "gloo (host)"),
-            "n_embd": hp["n_embd"], "n_layer": hp["n_layer"],
-            "ms_per_token": dt / args.steps_split * 1e3}
+    print(json.dumps({"stage": s, "layers": list(lr), "load_s": load_s, "decode_s": dec,
+                      "prefill_s": pre[args.split_micro], "prefill_nomicro_s": pre[0]}), flush=True)
+
+
+def layer_split(args, rank, ws, local, pg):
+    """N > 1: LLaMA-65B Q4_0 (BASELINE configs[4]) split by layers over the ws ranks, one
+    stage per GPU, residual stream over RCCL send/recv (the C++ stage link).  Each rank runs
+    its stage in a child process under a time limit, so a transport failure costs this line,
+    not the bench."""
+    path = args.split_model or os.path.join(os.path.dirname(args.model), "llama-65b-q4_0.bin")
+    ensure_model(path, rank, pg, CFG_65B)
+    import lvk
+    uid = [lvk.rccl_unique_id().hex() if rank == 0 else None]
+    if pg is not None:
+        pg.broadcast_object_list(uid, src=0)
+    cmd = [sys.executable, os.path.abspath(__file__), "--split-child", "--split-stages", str(ws),
+           "--split-stage", str(rank), "--split-device", str(local % lvk.device_count()), "--split-uid", uid[0],
+           "--split-model", path, "--steps-split", str(args.steps_split), "--warmup", "4",
+           "--split-micro", str(args.split_micro)]
+    res, err = None, None
+    try:
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=SPLIT_TIMEOUT_S)
+        if p.returncode == 0:
+            res = json.loads(p.stdout.decode().strip().splitlines()[-1])
+        else:
+            err = "rank %d stage exited %d: %s" % (rank, p.returncode, p.stderr.decode(errors="replace")[-400:])
+    except subprocess.TimeoutExpired:
+        err = "rank %d stage timed out after %d s" % (rank, SPLIT_TIMEOUT_S)
+    except Exception as e:                       # noqa: BLE001 -- reported in the line
+        err = "rank %d: %r" % (rank, e)
+    ok = all_max(pg, 0.0 if res is not None else 1.0) == 0.0
+    if not ok:
+        errs = [err]
+        if pg is not None:
+            errs = [None] * ws
+            pg.all_gather_object(errs, err)
+        return {"error": [e for e in errs if e]}
+    dec = all_max(pg, res["decode_s"])
+    pre = all_max(pg, res["prefill_s"])
+    pre0 = all_max(pg, res["prefill_nomicro_s"])
+    L = CFG_65B["n_layer"]
+    r = args.steps_split / dec
+    return {"value": r, "unit": "tok/s", "stages": ws, "steps": args.steps_split, "ms_per_token": 1e3 / r,
+            "layers_per_stage": [[s * L // ws, (s + 1) * L // ws] for s in range(ws)],
+            "workload": "LLaMA-65B Q4_0 (synthetic, seed 3) greedy decode, layers split over %d GPUs (one stage "
+                        "per rank, C++ stage link: ncclRecv -> layers -> ncclSend of inpL f32 [n_embd] on the "
+                        "stage stream, greedy token relayed last -> first by ncclSend), n_ctx 512" % ws,
+            "frac_hbm_roofline_1gpu": r * MODEL_BYTES_65B / 1e9 / HBM_PEAK_GBS,
+            "prefill_512": {"tok_s": 512 / pre, "ms": pre * 1e3, "micro_batch": args.split_micro,
+                            "tok_s_no_micro_batch": 512 / pre0},
+            "transport": "RCCL (ncclCommInitRank over the %d ranks)" % ws}
 
 
 def decode_65b(args, rank, pg, n_ctx, ptoks):
@@ -275,13 +326,22 @@ def main():
     ap.add_argument("--no-65b", action="store_true", help="skip the 1-GPU 65B decode line (BASELINE configs[4], S=1)")
     ap.add_argument("--steps-65b", type=int, default=32)
     ap.add_argument("--no-split", action="store_true", help="N>1: skip the layer-split pipeline line (SURVEY 8e)")
-    ap.add_argument("--steps-split", type=int, default=64)
-    ap.add_argument("--split-model", default=None, help="model for the layer-split line (default: the 7B file)")
-    ap.add_argument("--split-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="stage hand-off transport: RCCL on device buffers, or gloo through host memory")
+    ap.add_argument("--steps-split", type=int, default=48)
+    ap.add_argument("--split-model", default=None, help="model for the layer-split line (default: the 65B file)")
+    ap.add_argument("--split-micro", type=int, default=64, help="prompt micro-batch of the layer split (tokens)")
+    ap.add_argument("--split-rehearse", action="store_true",
+                    help="run the layer-split leg at N = 1 too (one stage: the RCCL link on one rank)")
+    ap.add_argument("--split-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--split-stages", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--split-stage", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--split-device", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--split-uid", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
     args = ap.parse_args()
+    if args.split_child:
+        split_child(args)
+        return
 
     ws, rank, local, pg = dist_setup()
     n_gpus = args.gpus if args.gpus else ws
@@ -408,12 +468,6 @@ def main():
                 "avg_launch_us": avg_s * 1e6}
     step_gbs = value / n_gpus * MODEL_BYTES_7B / 1e9
 
-    # N > 1: the same 7B model split by layers over the ranks (SURVEY.md 8e
-    # pipeline: RCCL send/recv of the residual stream between stages)
-    split = None
-    if ws > 1 and not args.no_split:
-        split = layer_split_decode(args, m, rank, ws, local, pg, n_ctx, ptoks)
-
     # 13B Q4_1 single-stream decode (BASELINE.json configs[3]), same loop
     m.close()          # one model resident at a time from here on
     q41 = None
@@ -439,6 +493,11 @@ def main():
                "model_bytes_per_token": MODEL_BYTES_13B_Q41,
                "frac_hbm_roofline": r13 * MODEL_BYTES_13B_Q41 / 1e9 / HBM_PEAK_GBS,
                "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_13B_Q41}
+    # N > 1: LLaMA-65B split by layers over the ranks (RCCL send/recv of
+    # the residual stream between stages)
+    split = None
+    if (ws > 1 or args.split_rehearse) and not args.no_split:
+        split = layer_split(args, rank, ws, local, pg)
     d65 = None
     if ws == 1 and not args.no_65b:
         d65 = decode_65b(args, rank, pg, n_ctx, ptoks)

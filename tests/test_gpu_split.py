@@ -157,3 +157,23 @@ def test_split_shapes_vs_oracle(lvk, oracle, model_dir, cfg, stages, micro):
         tok = int(np.argmax(a[-1]))
     m.close()
     om.close()
+
+
+def test_stage_link_single_rank(lvk, tiny_models):
+    """the one-stage-per-process link (lvk_rccl_unique_id / lvk_stage_connect /
+    lvk_stage_step, what bench.py's layer-split ranks run) with one rank: RCCL loads, the
+    communicator forms, and prompt micro-batches + greedy steps equal the plain context"""
+    path = tiny_models["tiny_q4_0"]
+    ref = lvk.Llama(path, n_ctx=128)
+    want, wt = run(ref, PROMPT, 10)
+    ref.close()
+    st = lvk.Llama(path, n_ctx=128, layers=(0, lvk.model_hparams(path)["n_layer"]))
+    st.stage_connect(lvk.rccl_unique_id(), 1, 0)
+    assert st.stage_step(PROMPT, len(PROMPT), 0, micro=7) == 0
+    assert np.array_equal(bits(st.logits()[-1]), bits(want[0][-1]))
+    tok, got = wt[0], [wt[0]]
+    for i in range(10):
+        tok = st.stage_step([tok], 1, len(PROMPT) + i, greedy=True)
+        got.append(tok)
+    assert got == wt
+    st.close()
