@@ -114,11 +114,15 @@ hipError_t launch_matvec(const MvLaunch & L, int pro, int epi, hipStream_t s);
 // the same for Q4_1 weights (matvec_q41.hip); launch_matvec forwards here
 hipError_t launch_matvec_q41(const MvLaunch & L, int pro, int epi, hipStream_t s);
 
-// single-token decode matvec, one workgroup per CU (matvec_cu.hip).  Row
-// lengths compiled in: matvec_cu_supported(K).  Returns hipErrorNotSupported
-// for anything else (the caller then uses launch_matvec).
-bool matvec_cu_supported(int K);
+// single-token decode matvec, one workgroup per CU (matvec_cu.hip for Q4_0,
+// matvec_cu41.hip for Q4_1).  Row lengths compiled in: matvec_cu_supported(K, qtype).
+// Returns hipErrorNotSupported for anything else (the caller then uses launch_matvec).
+bool matvec_cu_supported(int K, int qtype = Q4_0);
 hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s);
+bool matvec_cu41_supported(int K);
+hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t s);
+// compute units of the current device (one decode workgroup per CU)
+int cu_count();
 
 // token embedding rows: x[t] = dequant(tok_emb[tokens[t]]) (ggml.c:6868-6895)
 hipError_t launch_embed(const void * emb, int emb_type, int n_embd, const int * tokens, int n,

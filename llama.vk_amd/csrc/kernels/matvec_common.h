@@ -136,5 +136,61 @@ __device__ __forceinline__ void q41_block_lds(const float * xb, int k, float & d
     qword = q41_pack8(v, mm.mn, id);
 }
 
+// ---- Q4_1 pieces shared by matvec_q41.hip and matvec_cu41.hip
+
+// quantize_row_q4_1 of one block held by a lane quad (lane k: elements 8k..8k+7)
+__device__ __forceinline__ void q41_quad(const float v[8], float & d, float & m, uint32_t & qword) {
+    float cm[8], cn[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        const float a0 = quad_bcast<0>(v[l]), a1 = quad_bcast<1>(v[l]);
+        const float a2 = quad_bcast<2>(v[l]), a3 = quad_bcast<3>(v[l]);
+        float x = a0 > a1 ? a0 : a1;  x = x > a2 ? x : a2;  x = x > a3 ? x : a3;
+        float n = a0 < a1 ? a0 : a1;  n = n < a2 ? n : a2;  n = n < a3 ? n : a3;
+        cm[l] = x; cn[l] = n;
+    }
+    const MinMax mm = q41_tree(cm, cn);
+    d = (mm.mx - mm.mn) / 15.0f;                          // ggml.c:874
+    const float id = d != 0.0f ? 1.0f / d : 0.0f;         // ggml.c:875
+    m = mm.mn;
+    qword = q41_pack8(v, mm.mn, id);
+}
+
+// Q4_1 activation table of one token:
+//   act[nb/4][8] uint4 : {a(4u,j), a(4u+1,j) << 16, a(4u+2,j), a(4u+3,j) << 16}
+//   dyv, myv [NC][8][4] : d / m of block 32c + 8m + j at [c][j][m]
+//   ysum[nb/4][4 q][4]  : sum of the 8 nibbles 8q..8q+7 of block 4u+t at [u][q][t]
+__device__ __forceinline__ void act41_store(uint32_t * act, float * dyv, float * myv, float * ysum, int i,
+                                            const uint32_t qs[4], float d, float m) {
+    const int slot = i & 3;
+    const uint32_t sh = (slot & 1) ? 16u : 0u;
+    uint32_t * base = act + (size_t) (i >> 2) * 32;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t lo = (qs[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+        const uint32_t hi = (qs[2 + (j >> 2)] >> (8 * (j & 3))) & 0xFFu;
+        base[j * 4 + slot] = (lo | (hi << 8)) << sh;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ysum[(size_t) (i >> 2) * 16 + q * 4 + slot] = (float) udot8(qs[q], 0x11111111u);
+    const int o = (i >> 5) * 32 + (i & 7) * 4 + ((i >> 3) & 3);
+    dyv[o] = d;
+    myv[o] = m;
+}
+
+// even-chain weight sums of two blocks packed in one weight word (low 16 bits
+// block A, high 16 bits block B; each 16-bit group = [qs byte j, qs byte 8+j]).
+// Quad 0 of a row holds chains 0-3 (first bytes: elements 0-7, second bytes:
+// 16-23), quad 1 chains 4-7 (8-15, 24-31); chain 2q needs elements 8q..8q+7:
+// j=0 own quad first, j=2 other quad first, j=4 other quad second, j=6 own
+// quad second.  Returns {S_A, S_B} in the low/high 16 bits (odd lanes: junk).
+__device__ __forceinline__ uint32_t wsum_word(uint32_t w, bool other, uint32_t shift) {
+    uint32_t t = (w & 0x0F0F0F0Fu) + ((w >> 4) & 0x0F0F0F0Fu);                  // per byte: its 2 nibbles
+    t += (uint32_t) __builtin_amdgcn_mov_dpp((int) t, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    t += (uint32_t) __builtin_amdgcn_mov_dpp((int) t, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    const uint32_t mir = (uint32_t) __builtin_amdgcn_mov_dpp((int) t, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    return ((other ? mir : t) >> shift) & 0x00FF00FFu;
+}
+
 }  // namespace mv
 }  // namespace lvk

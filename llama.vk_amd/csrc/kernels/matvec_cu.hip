@@ -407,18 +407,6 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
 
 // -- host -------------------------------------------------------------------
 
-int cu_count() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess) return 256;
-        hipDeviceProp_t p;
-        if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 256;
-        n = p.multiProcessorCount;
-    }
-    return n;
-}
-
 template <int NW, int NP, int D, int PRO, int EPI, int KT>
 hipError_t go(const CuParams & P, hipStream_t s) {
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
@@ -433,14 +421,30 @@ hipError_t go(const CuParams & P, hipStream_t s) {
 
 }  // namespace
 
+int cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return 256;
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 256;
+        n = p.multiProcessorCount;
+    }
+    return n;
+}
+
 #ifdef LVK_PROBE_TIMING
 void * lvk_probe_trace() { void * p = nullptr; (void) hipGetSymbolAddress(&p, HIP_SYMBOL(g_trace)); return p; }
 #endif
 // row lengths compiled in: the LLaMA 7B/13B-free Q4_0 shapes (n_embd 4096 / 8192,
 // n_ff 11008 / 22016; llama.cpp:771-779)
-bool matvec_cu_supported(int K) { return K == 4096 || K == 11008 || K == 8192 || K == 22016; }
+bool matvec_cu_supported(int K, int qtype) {
+    if (qtype == Q4_1) return matvec_cu41_supported(K);
+    return K == 4096 || K == 11008 || K == 8192 || K == 22016;
+}
 
 hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s) {
+    if (L.w.qtype == Q4_1) return launch_matvec_cu41(L, pro, epi, s);
     if (L.w.qtype != Q4_0 || L.n_tokens != 1 || L.w.M % 8) return hipErrorNotSupported;
     CuParams P{};
     P.nib = L.w.nib;

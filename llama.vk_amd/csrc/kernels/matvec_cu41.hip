@@ -1,0 +1,410 @@
+// matvec_cu41.hip -- CU-balanced single-token Q4_1 matvec (the 13B Q4_1 decode path).
+//
+// The streaming skeleton of matvec_cu.hip (one workgroup per CU, each CU owns an equal
+// share of the 8-row groups, every wave keeps D chunks of its weight stream in flight
+// across group boundaries, the activation table built in LDS while the first chunks
+// are already in flight) with the Q4_1 arithmetic of matvec_q41.hip:
+//
+//   ggml_vec_dot_q4_1 AVX2 (ggml.c:2188-2258), x = weight row, y = activation,
+//   per block i in order and chain j = 0..7:
+//     acc_j = fmaf(dx*dy, (float) p_j, acc_j)
+//     acc_j = fmaf(j even ? dx*my : mx*dy, (float) S_j, acc_j)
+//     off   = off + mx*my
+//   result = hsum(acc) + off * 32
+//
+// on an activation quantized by quantize_row_q4_1 (ggml.c:847-920).  One chunk of
+// the image is 8 rows x 32 blocks: 4 KiB of nibbles + 1 KiB of d + 1 KiB of m (24 B
+// per 32 weights, the file's bytes).  Row lengths are template constants (the 13B
+// shapes 5120 / 13824 and the 7B shapes 4096 / 11008), so every load is exact and
+// static.
+#include "lvk_device.h"
+#include "lvk_kernels.h"
+#include "matvec_common.h"
+
+namespace lvk {
+
+namespace {
+using namespace mv;
+
+struct Cu41Params {
+    const uint4 * nib;
+    const float4 * scl;         // [G][NC][2][64]: d, then m
+    int G;                      // row groups (M / 8)
+    const float * x;            // PRO_NORM / PRO_ACTF: f32 input [K]
+    const float * g;            // PRO_NORM: norm weight [K]
+    ActQ xq;                    // PRO_ACTQ: quantized input (d, m, qs)
+    const StepParams * sp;
+    float * y;                  // EPI_STORE / EPI_RESID
+    float * u;                  // EPI_SWIGLU_F32: silu(w1 x) * (w3 x) [M/2]
+    uint16_t * q16;
+    uint16_t * kc;
+    uint16_t * vc;
+    const float2 * rope;
+    int n_embd, head_dim, n_ctx;
+    const uint16_t * silu_tab;
+};
+
+template <int NW, int D, int PRO, int EPI, int KT>
+__global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
+    constexpr int nb = KT / 32;                 // blocks per row
+    constexpr int nsub = nb / 8;                // 8-block sub-chunks (one uint4 per lane each)
+    constexpr int NC = (nb + 31) / 32;          // chunks of 32 blocks
+    constexpr bool XG = (NC % D) == 0;          // prefetch may cross into the next group
+    constexpr int nunits = KT / 8;              // f32 prologue work units (8 elements)
+    constexpr int NT = NW * 64;
+    static_assert(D <= NC, "prefetch deeper than a row");
+    static_assert(nb % 8 == 0, "K must be a multiple of 256");
+
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t * act = (uint32_t *) smem;                          // nb * 32 B
+    float * dyv = (float *) (smem + nb * 32);                    // NC * 32
+    float * myv = dyv + NC * 32;                                 // NC * 32
+    float * ys = myv + NC * 32;                                  // nb * 4
+    float * sbuf = ys + nb * 4;                                  // NW * 1024
+    double * red = (double *) (sbuf + NW * 1024);                // NW
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 7;
+    const int r = lane >> 3;
+    const int nwg = gridDim.x;
+    const int g0 = (int) (blockIdx.x * (unsigned) P.G / (unsigned) nwg);
+    const int g1 = (int) ((blockIdx.x + 1) * (unsigned) P.G / (unsigned) nwg);
+    const int ng = max(0, (g1 - g0 - wave + NW - 1) / NW);      // row groups of this wave
+    int gc = min(g0 + wave, P.G - 1);
+
+    // activation inputs first (vmcnt retires in order)
+    constexpr bool FPRO = (PRO == PRO_NORM || PRO == PRO_ACTF);
+    constexpr int UM = FPRO ? (nunits + NT - 1) / NT : (nb + NT - 1) / NT;
+    float4 xv[UM][2];
+    float4 gv[PRO == PRO_NORM ? UM : 1][2];
+    uint4 qv[FPRO ? 1 : UM];
+    float dv[FPRO ? 1 : UM], mv_[FPRO ? 1 : UM];
+    if constexpr (FPRO) {
+#pragma unroll
+        for (int k = 0; k < UM; ++k) {
+            const int un = min(k * NT + tid, nunits - 1);
+            const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
+            xv[k][0] = xp[0]; xv[k][1] = xp[1];
+            if constexpr (PRO == PRO_NORM) {
+                const float4 * gp = (const float4 *) (P.g + (size_t) un * 8);
+                gv[k][0] = gp[0]; gv[k][1] = gp[1];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < UM; ++k) {
+            const int b = min(k * NT + tid, nb - 1);
+            qv[k] = P.xq.qs[b];
+            dv[k] = P.xq.d[b];
+            mv_[k] = P.xq.m[b];
+        }
+    }
+
+    // first D chunks of this wave's first row group (scalar-base loads)
+    const uint32_t loff = ng > 0 ? (uint32_t) lane * 16u : 0u;
+    uint4 W[D][4];
+    float4 SD[D], SM[D];
+#define LVK_ISSUE41(slot, grp, cc)                                                                      \
+    do {                                                                                                \
+        const uint4 * nb_ = P.nib + ((size_t) (grp) * NC * 4 + (cc) * 4) * 64;                          \
+        _Pragma("unroll") for (int sb = 0; sb < 4; ++sb) if ((cc) * 4 + sb < nsub)                      \
+            W[slot][sb] = ld_nt((const uint4 *) ((const char *) (nb_ + sb * 64) + loff));               \
+        const char * sc_ = (const char *) (P.scl + ((size_t) (grp) * NC + (cc)) * 128) + loff;          \
+        SD[slot] = *(const float4 *) sc_;                                                               \
+        SM[slot] = *(const float4 *) (sc_ + 1024);                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                              \
+    } while (0)
+#pragma unroll
+    for (int d = 0; d < D; ++d) LVK_ISSUE41(d, gc, d);
+
+    // activation table
+    if constexpr (FPRO) {
+        float scale = 1.0f;
+        if constexpr (PRO == PRO_NORM) {
+            // ggml_compute_forward_rms_norm_f32 (ggml.c:6058-6076): float squares summed
+            // in double; per-thread units, a DPP wave tree, the NW wave sums in order
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < UM; ++k) {
+                if (k * NT + tid < nunits) {
+                    const float e[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
+                                        xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) { const float sq = e[q] * e[q]; acc += (double) sq; }
+                }
+            }
+            acc = wave_sum_d(acc);
+            if (lane == 0) red[wave] = acc;
+            __syncthreads();
+            double sum = red[0];
+            for (int w = 1; w < NW; ++w) sum += red[w];
+            const float mean = (float) (sum / (double) KT);
+            scale = 1.0f / sqrtf(mean + 1e-6f);
+        }
+#pragma unroll
+        for (int k = 0; k < UM; ++k) {
+            if (k * NT >= nunits) break;
+            const int un = k * NT + tid;
+            float v[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
+                          xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
+            if constexpr (PRO == PRO_NORM) {
+                const float gg[8] = {gv[k][0].x, gv[k][0].y, gv[k][0].z, gv[k][0].w,
+                                     gv[k][1].x, gv[k][1].y, gv[k][1].z, gv[k][1].w};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float yn = v[e] * scale;      // ggml_vec_scale_f32 (ggml.c:6076)
+                    v[e] = gg[e] * yn;                  // ggml_mul(repeat(g), cur) (llama.cpp:984)
+                }
+            }
+            // the 4 units of a block are a lane quad (nunits % 4 == 0, NT % 4 == 0)
+            float d, m;
+            uint32_t qw;
+            q41_quad(v, d, m, qw);
+            uint32_t qs[4];
+            qs[0] = __builtin_bit_cast(uint32_t, quad_bcast<0>(__builtin_bit_cast(float, qw)));
+            qs[1] = __builtin_bit_cast(uint32_t, quad_bcast<1>(__builtin_bit_cast(float, qw)));
+            qs[2] = __builtin_bit_cast(uint32_t, quad_bcast<2>(__builtin_bit_cast(float, qw)));
+            qs[3] = __builtin_bit_cast(uint32_t, quad_bcast<3>(__builtin_bit_cast(float, qw)));
+            if (un < nunits && (un & 3) == 0) act41_store(act, dyv, myv, ys, un >> 2, qs, d, m);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < UM; ++k) {
+            const int b = k * NT + tid;
+            if (b < nb) {
+                const uint32_t qs[4] = {qv[k].x, qv[k].y, qv[k].z, qv[k].w};
+                act41_store(act, dyv, myv, ys, b, qs, dv[k], mv_[k]);
+            }
+        }
+    }
+    __syncthreads();            // activation table ready
+    if (ng == 0) return;
+
+    // row groups: chunk loop with cross-group prefetch
+    const bool even = (j & 1) == 0;
+    const bool other = (j == 2 || j == 4);
+    const uint32_t wsh = j >= 4 ? 8u : 0u;
+    float * sw = sbuf + wave * 1024;
+    auto body = [&](auto has_next, int grp, int gnext, float & off) __attribute__((always_inline)) {
+        float acc = 0.0f;
+        off = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int slot = c % D;
+            {
+                // products of blocks 32c + 8m + j of this lane's row (ggml.c:2205-2212):
+                // s = dx*dy, ce = dx*my, co = mx*dy, mm = mx*my; slot 8m + j = block 32c + 8m + j
+                const float4 dy = *(const float4 *) (dyv + c * 32 + j * 4);
+                const float4 my = *(const float4 *) (myv + c * 32 + j * 4);
+                float * sl = sw + r * 32 + j;
+                const float dxa[4] = {SD[slot].x, SD[slot].y, SD[slot].z, SD[slot].w};
+                const float mxa[4] = {SM[slot].x, SM[slot].y, SM[slot].z, SM[slot].w};
+                const float dya[4] = {dy.x, dy.y, dy.z, dy.w};
+                const float mya[4] = {my.x, my.y, my.z, my.w};
+#pragma unroll
+                for (int mq = 0; mq < 4; ++mq) {
+                    sl[mq * 8] = dxa[mq] * dya[mq];
+                    sl[256 + mq * 8] = dxa[mq] * mya[mq];
+                    sl[512 + mq * 8] = mxa[mq] * dya[mq];
+                    sl[768 + mq * 8] = mxa[mq] * mya[mq];
+                }
+                __builtin_amdgcn_wave_barrier();
+                const float * srow = sw + r * 32;
+                const float * xrow = srow + (even ? 256 : 512);
+                const float * mrow = srow + 768;
+#pragma unroll
+                for (int sb = 0; sb < 4; ++sb) {
+                    if (c * 4 + sb < nsub) {
+                        const uint32_t wd[4] = {W[slot][sb].x, W[slot][sb].y, W[slot][sb].z, W[slot][sb].w};
+#pragma unroll
+                        for (int pp = 0; pp < 2; ++pp) {
+                            const int uu = c * 8 + sb * 2 + pp;           // group of 4 blocks
+                            const int bi = sb * 8 + pp * 4;               // first block within chunk
+                            const uint4 a = *(const uint4 *) (act + ((size_t) uu * 8 + j) * 4);
+                            const float4 s4 = *(const float4 *) (srow + bi);
+                            const float4 x4 = *(const float4 *) (xrow + bi);
+                            const float4 m4 = *(const float4 *) (mrow + bi);
+                            const float4 y4 = *(const float4 *) (ys + (size_t) uu * 16 + (j >> 1) * 4);
+                            const uint32_t w01 = wsum_word(wd[2 * pp], other, wsh);
+                            const uint32_t w23 = wsum_word(wd[2 * pp + 1], other, wsh);
+                            const float S[4] = {even ? (float) (w01 & 0xFFFFu) : y4.x, even ? (float) (w01 >> 16) : y4.y,
+                                                even ? (float) (w23 & 0xFFFFu) : y4.z, even ? (float) (w23 >> 16) : y4.w};
+                            const int p[4] = {udot8(wd[2 * pp], a.x), udot8(wd[2 * pp], a.y),
+                                              udot8(wd[2 * pp + 1], a.z), udot8(wd[2 * pp + 1], a.w)};
+                            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+                            const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+                            const float ms[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                acc = __builtin_fmaf(sv[k], (float) p[k], acc);
+                                acc = __builtin_fmaf(xs[k], S[k], acc);
+                                off = off + ms[k];
+                            }
+                        }
+                    }
+                }
+            }
+            if (c + D < NC) LVK_ISSUE41(slot, grp, c + D);
+            else if constexpr (decltype(has_next)::value && XG) LVK_ISSUE41(slot, gnext, c + D - NC);
+            // chunks stay in program order; the product buffer is rewritten by the next chunk
+            asm volatile("" : "+v"(acc), "+v"(off));
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return octet_reduce(acc);
+    };
+
+    auto epilogue = [&](int grp, float h, float off) __attribute__((always_inline)) {
+        const float res = h + off * 32.0f;        // acc_offset * QK (ggml.c:2249)
+        const int row = grp * 8 + r;
+        if constexpr (EPI == EPI_STORE) {
+            if (j == 0) P.y[row] = res;
+        } else if constexpr (EPI == EPI_RESID) {
+            if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+        } else if constexpr (EPI == EPI_QKV) {
+            const int E = P.n_embd, hd = P.head_dim;
+            const int which = row / E;          // 0 q, 1 k, 2 v (uniform per wave: E % 8 == 0)
+            const int e = row - which * E;
+            const int pos = P.sp->n_past;
+            const float other_r = __shfl_xor(res, 8);   // row e^1 lives in lanes of row r^1
+            if (j == 0) {
+                if (which < 2) {
+                    // ggml_compute_forward_rope_f32 mode 0 (ggml.c:7209-7223)
+                    const int i0 = e % hd;
+                    const float2 cs = P.rope[(size_t) pos * (hd / 2) + (i0 >> 1)];
+                    float out;
+                    if ((i0 & 1) == 0) { const float a = res * cs.x, b = other_r * cs.y; out = a - b; }
+                    else               { const float a = other_r * cs.y, b = res * cs.x; out = a + b; }
+                    if (which == 0) P.q16[e] = f32_to_f16(out);
+                    else            P.kc[(size_t) pos * E + e] = f32_to_f16(out);
+                } else {
+                    P.vc[(size_t) e * P.n_ctx + pos] = f32_to_f16(res);
+                }
+            }
+        } else if constexpr (EPI == EPI_SWIGLU_F32) {
+            // fused W1|W3 image interleaved per 4 rows: rows 0-3 of the group are
+            // w1 rows 4grp..4grp+3, rows 4-7 the w3 rows (llama.cpp:1085-1096)
+            const float a3 = __shfl_xor(res, 32);
+            if (r < 4 && j == 0) {
+                const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res)]);   // ggml_vec_silu_f32 (ggml.c:2495)
+                P.u[grp * 4 + r] = sl * a3;                                  // ggml_mul (llama.cpp:1096)
+            }
+        }
+    };
+
+    if constexpr (XG) {
+        for (int k = 0; k + 1 < ng; ++k) {
+            float off;
+            const float h = body(std::true_type{}, gc, gc + NW, off);
+            epilogue(gc, h, off);
+            gc += NW;
+        }
+    }
+    float off;
+    const float h = body(std::false_type{}, gc, gc, off);
+    epilogue(gc, h, off);
+#undef LVK_ISSUE41
+}
+
+template <int NW, int D, int PRO, int EPI, int KT>
+hipError_t go(const Cu41Params & P, hipStream_t s) {
+    constexpr int nb = KT / 32, NC = (nb + 31) / 32;
+    constexpr bool XG = (NC % D) == 0;
+    const int nwg = std::min(cu_count(), P.G);
+    // without cross-group prefetch every wave must own at most one group
+    if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
+    const size_t lds = (size_t) nb * 32 + 2 * NC * 128 + (size_t) nb * 16 + NW * 4096 + NW * 8;
+    LVK_LAUNCH((k_mv_cu41<NW, D, PRO, EPI, KT>), dim3(nwg), dim3(NW * 64), lds, s, P);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool matvec_cu41_supported(int K) { return K == 4096 || K == 5120 || K == 11008 || K == 13824; }
+
+hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t s) {
+    if (L.w.qtype != Q4_1 || L.n_tokens != 1 || L.w.M % 8) return hipErrorNotSupported;
+    Cu41Params P{};
+    P.nib = L.w.nib;
+    P.scl = (const float4 *) L.w.scl;
+    P.G = L.w.M / 8;
+    P.x = L.x ? L.x + (size_t) L.tok0 * L.w.K : nullptr;
+    P.g = L.g;
+    P.xq = L.xq;
+    if (P.xq.qs) {
+        P.xq.qs += (size_t) L.tok0 * L.xq.nb;
+        P.xq.d += (size_t) L.tok0 * L.xq.nb;
+        P.xq.m += (size_t) L.tok0 * L.xq.nb;
+    }
+    P.sp = L.sp;
+    P.y = L.y ? L.y + (size_t) L.out_tok0 * L.w.M : nullptr;
+    P.u = L.u;
+    P.q16 = L.q16; P.kc = L.kc; P.vc = L.vc; P.rope = L.rope.cs;
+    P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx;
+    P.silu_tab = L.silu_tab;
+    const int K = L.w.K;
+#ifdef LVK_PROBE_SWEEP   // dev probe builds only: LVK_CFG41 selects a launch shape
+    {
+        static int cfg = getenv("LVK_CFG41") ? atoi(getenv("LVK_CFG41")) : 0;
+        if (K == 5120 && epi == EPI_QKV) {
+            if (cfg == 1) return go<8, 3, PRO_NORM, EPI_QKV, 5120>(P, s);
+            if (cfg == 2) return go<4, 5, PRO_NORM, EPI_QKV, 5120>(P, s);
+            if (cfg == 3) return go<16, 2, PRO_NORM, EPI_QKV, 5120>(P, s);
+        }
+        if (K == 5120 && epi == EPI_SWIGLU_F32) {
+            if (cfg == 1) return go<8, 5, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
+            if (cfg == 2) return go<14, 3, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
+            if (cfg == 3) return go<16, 1, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
+        }
+        if (K == 5120 && epi == EPI_RESID) {
+            if (cfg == 1) return go<3, 5, PRO_ACTQ, EPI_RESID, 5120>(P, s);
+            if (cfg == 2) return go<4, 3, PRO_ACTQ, EPI_RESID, 5120>(P, s);
+            if (cfg == 3) return go<2, 5, PRO_ACTQ, EPI_RESID, 5120>(P, s);
+        }
+        if (K == 13824 && epi == EPI_RESID) {
+            if (cfg == 1) return go<4, 7, PRO_ACTF, EPI_RESID, 13824>(P, s);
+            if (cfg == 2) return go<3, 2, PRO_ACTF, EPI_RESID, 13824>(P, s);
+            if (cfg == 3) return go<2, 7, PRO_ACTF, EPI_RESID, 13824>(P, s);
+        }
+        if (K == 5120 && epi == EPI_STORE && pro == PRO_NORM) {
+            if (cfg == 1) return go<8, 5, PRO_NORM, EPI_STORE, 5120>(P, s);
+            if (cfg == 2) return go<16, 1, PRO_NORM, EPI_STORE, 5120>(P, s);
+        }
+    }
+#endif
+    // launch shapes per row length and role: waves such that every CU keeps ~60-120 KB
+    // of weights in flight (K = 5120: NC = 5 chunks per row, so D = 2 does not divide
+    // the row and every wave owns at most one 8-row group)
+    if (K == 5120) {
+        switch (epi) {
+            case EPI_QKV: if (pro == PRO_NORM) return go<8, 2, PRO_NORM, EPI_QKV, 5120>(P, s); break;
+            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<14, 2, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s); break;
+            case EPI_STORE:
+                if (pro == PRO_NORM) return go<16, 2, PRO_NORM, EPI_STORE, 5120>(P, s);
+                if (pro == PRO_ACTF) return go<16, 2, PRO_ACTF, EPI_STORE, 5120>(P, s);
+                break;
+            case EPI_RESID: if (pro == PRO_ACTQ) return go<3, 2, PRO_ACTQ, EPI_RESID, 5120>(P, s); break;
+        }
+    } else if (K == 13824) {
+        if (epi == EPI_RESID && pro == PRO_ACTF) return go<4, 2, PRO_ACTF, EPI_RESID, 13824>(P, s);
+        if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 2, PRO_ACTF, EPI_STORE, 13824>(P, s);
+    } else if (K == 4096) {
+        switch (epi) {
+            case EPI_QKV: if (pro == PRO_NORM) return go<8, 2, PRO_NORM, EPI_QKV, 4096>(P, s); break;
+            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<8, 2, PRO_NORM, EPI_SWIGLU_F32, 4096>(P, s); break;
+            case EPI_STORE:
+                if (pro == PRO_NORM) return go<8, 2, PRO_NORM, EPI_STORE, 4096>(P, s);
+                if (pro == PRO_ACTF) return go<8, 2, PRO_ACTF, EPI_STORE, 4096>(P, s);
+                break;
+            case EPI_RESID: if (pro == PRO_ACTQ) return go<2, 2, PRO_ACTQ, EPI_RESID, 4096>(P, s); break;
+        }
+    } else if (K == 11008) {
+        if (epi == EPI_RESID && pro == PRO_ACTF) return go<4, 4, PRO_ACTF, EPI_RESID, 11008>(P, s);
+        if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 4, PRO_ACTF, EPI_STORE, 11008>(P, s);
+    }
+    return hipErrorNotSupported;
+}
+
+}  // namespace lvk

@@ -259,7 +259,7 @@ static double qbytes(const QMatrix & w) { return (double) w.M * (w.K / 32) * (w.
 // decode kernels: the CU-balanced path (matvec_cu.hip) where its row length is
 // compiled in, else the generic kernel
 static hipError_t mv_launch(const MvLaunch & L, int pro, int epi, hipStream_t s) {
-    if (L.n_tokens == 1 && matvec_cu_supported(L.w.K)) {
+    if (L.n_tokens == 1 && matvec_cu_supported(L.w.K, L.w.qtype)) {
         const hipError_t e = launch_matvec_cu(L, pro, epi, s);
         if (e != hipErrorNotSupported) return e;
     }
@@ -352,7 +352,7 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
         return;
     }
     // single-token FFN: W1|W3 hands silu(w1 x)*(w3 x) to W2 in f32, W2 quantizes it
-    const bool ffn_f32 = n == 1 && model.qtype == Q4_0 && matvec_cu_supported(E) && matvec_cu_supported(F);
+    const bool ffn_f32 = n == 1 && matvec_cu_supported(E, model.qtype) && matvec_cu_supported(F, model.qtype);
     // attention, Wo and the residual add in one launch (attention_decode.hip, k_attn_wo)
     const bool attn_wo = n == 1 && !old_attention && fuse_attn_wo && model.qtype == Q4_0 && !model.layers.empty() &&
                          attention_wo_supported(E, H, n_ctx, model.layers[0].wo);

@@ -100,7 +100,12 @@ static int mul_mat_impl(int type, const void * w, int m, int k, const float * g,
         // Q4_1 kernels quantize the f32 input in their prologue
         L.x = xd;
         if (norm) L.g = dv.up(g, (size_t) k);
-        LVK_HIP(lvk::launch_matvec(L, norm ? lvk::PRO_NORM : lvk::PRO_ACTF, lvk::EPI_STORE, nullptr));
+        const int pro = norm ? lvk::PRO_NORM : lvk::PRO_ACTF;
+        // single column: the CU-balanced decode kernel (matvec_cu41.hip) where compiled in
+        hipError_t e = hipErrorNotSupported;
+        if (n == 1 && lvk::matvec_cu_supported(k, lvk::Q4_1)) e = lvk::launch_matvec_cu(L, pro, lvk::EPI_STORE, nullptr);
+        if (e == hipErrorNotSupported) e = lvk::launch_matvec(L, pro, lvk::EPI_STORE, nullptr);
+        LVK_HIP(e);
     } else if (n == 1 && lvk::matvec_cu_supported(k)) {
         // single column: the decode kernel (matvec_cu.hip), quantizing in its prologue
         L.x = xd;

@@ -153,11 +153,15 @@ def test_7b_shaped_fused_attention_wo_matches(lvk, oracle, model_dir, monkeypatc
     om.close()
 
 
-def test_13b_shaped_q4_1_decode_vs_oracle(lvk, oracle, model_dir):
-    """LLaMA-13B layer shapes in Q4_1 (n_embd 5120, n_ff 13824, 40 heads), 1 layer:
-    Q4_1 quantizer + dot + attention output quantization on the GPU, bit-exact."""
+@pytest.mark.parametrize("cfg,steps", [(dict(n_embd=5120, n_head=40, n_layer=2, seed=11), 12),
+                                       (dict(n_embd=4096, n_head=32, n_layer=2, seed=12), 8)])
+def test_q4_1_shaped_decode_vs_oracle(lvk, oracle, model_dir, cfg, steps):
+    """LLaMA-13B (n_embd 5120, n_ff 13824, 40 heads) and 7B layer shapes in Q4_1, 2 layers:
+    Q4_1 quantizer, the CU-balanced Q4_1 decode matvecs (matvec_cu41.hip: QKV + RoPE, Wo,
+    W1|W3 -> f32 u, W2 quantizing u, lm_head) and the attention output quantization on
+    the GPU, bit-exact against the oracle over a prompt and `steps` decode positions."""
     from oracle_lib import gen_model
-    path = gen_model(os.path.join(model_dir, "w5120_l1_q41.bin"), n_embd=5120, n_head=40, n_layer=1, ftype=3, seed=11)
+    path = gen_model(os.path.join(model_dir, "w%d_l2_q41.bin" % cfg["n_embd"]), ftype=3, **cfg)
     m = lvk.Llama(path, n_ctx=256)
     om = oracle.model(path, 256)
     toks = np.array([1, 450, 4996, 17354, 1701, 29916], np.int32)
@@ -165,12 +169,18 @@ def test_13b_shaped_q4_1_decode_vs_oracle(lvk, oracle, model_dir):
     b = om.eval(toks, 0)
     assert np.array_equal(bits(a), bits(b))
     n_past, tok = len(toks), int(np.argmax(a[-1]))
-    for _ in range(6):
+    for _ in range(steps):
         a = m.eval([tok], n_past)
         b = om.eval([tok], n_past)
         assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past
         n_past += 1
         tok = int(np.argmax(a[-1]))
+    # every decode matrix ran on the CU-balanced kernels: one launch per matrix and layer
+    m.set_profiling(True)
+    m.reset_profile()
+    m.eval([tok], n_past)
+    pr = m.profile()
+    assert pr["qkv"]["launches"] == 2 and pr["wo"]["launches"] == 2 and pr["w2"]["launches"] == 2
     m.close()
     om.close()
 

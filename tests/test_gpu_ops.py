@@ -54,7 +54,8 @@ def test_mul_mat_q4_0(lvk, oracle, m, k, n):
     assert np.array_equal(bits(got), bits(want))
 
 
-@pytest.mark.parametrize("m,k,n", [(64, 256, 1), (32, 5120, 1), (16, 13824, 1), (48, 5120, 3), (16, 1024, 8)])
+@pytest.mark.parametrize("m,k,n", [(64, 256, 1), (32, 5120, 1), (16, 13824, 1), (48, 5120, 3), (16, 1024, 8),
+                                   (4104, 5120, 1), (264, 4096, 1), (40, 11008, 1)])
 def test_mul_mat_q4_1(lvk, oracle, m, k, n):
     rng = np.random.default_rng(m * 5 + k + n)
     wq = _weights(oracle, rng, m, k, 3)
@@ -65,7 +66,7 @@ def test_mul_mat_q4_1(lvk, oracle, m, k, n):
     assert np.array_equal(bits(got), bits(want))
 
 
-@pytest.mark.parametrize("m,k,n", [(64, 256, 1), (32, 5120, 1), (32, 5120, 5)])
+@pytest.mark.parametrize("m,k,n", [(64, 256, 1), (32, 5120, 1), (32, 5120, 5), (2056, 5120, 1), (136, 4096, 1)])
 def test_mul_mat_q4_1_rmsnorm_prologue(lvk, oracle, m, k, n):
     rng = np.random.default_rng(m + k * 7 + n)
     wq = _weights(oracle, rng, m, k, 3)

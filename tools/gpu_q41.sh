@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ops.py -k "q4_1" tests/test_gpu_model.py::test_q4_1_shaped_decode_vs_oracle > gpurun_out/t_q41.log 2>&1 || { tail -30 gpurun_out/t_q41.log; exit 1; }
+tail -3 gpurun_out/t_q41.log
+timeout -k 10 300 python -u tools/decode_speed.py 13b 64 > gpurun_out/sp13.log 2>&1
+for c in 1 2 3; do LVK_LIB=$PWD/llama.vk_amd/lib/sweep/libllama_vk_amd.so LVK_CFG41=$c timeout -k 10 200 python -u tools/decode_speed.py 13b 64 >> gpurun_out/sp13.log 2>&1 || exit 1; done
+cat gpurun_out/sp13.log | grep model
