@@ -320,7 +320,7 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=48)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-greedy", action="store_true",
-                    help="skip the lvk_eval_greedy decode leg (rocprofv3 kernel-trace runs, DESIGN.md section 9)")
+                    help="skip the lvk_eval_greedy decode leg")
     ap.add_argument("--no-13b", action="store_true", help="skip the 13B Q4_1 decode line (BASELINE configs[3])")
     ap.add_argument("--steps-13b", type=int, default=96)
     ap.add_argument("--no-65b", action="store_true", help="skip the 1-GPU 65B decode line (BASELINE configs[4], S=1)")

@@ -263,5 +263,6 @@ namespace lvk {
 // y[t] = g * rms_norm(x[t]) as f32 (the embeddings output, llama.cpp:1117-1124)
 hipError_t launch_rmsnorm_rows(const float * x, const float * g, int K, int n, float * y, hipStream_t s);
 // greedy argmax over x[0..n) with the reference's first-maximum rule (llama.cpp:1382-1394); *out on the device
-hipError_t launch_argmax(const float * x, int n, int * out, hipStream_t s);
+// (out2, optional: a second copy of the token, e.g. host-mapped memory)
+hipError_t launch_argmax(const float * x, int n, int * out, hipStream_t s, int * out2 = nullptr);
 }  // namespace lvk

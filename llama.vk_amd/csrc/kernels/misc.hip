@@ -257,7 +257,8 @@ __device__ inline ArgBest arg_pick(ArgBest a, ArgBest b) {
     if (a.i == INT_MAX) return b;
     return (b.v > a.v || (b.v == a.v && b.i < a.i)) ? b : a;
 }
-__global__ __launch_bounds__(1024) void k_argmax_first(const float * __restrict__ x, int n, int * __restrict__ out) {
+__global__ __launch_bounds__(1024) void k_argmax_first(const float * __restrict__ x, int n, int * __restrict__ out,
+                                                       int * __restrict__ out2) {
     __shared__ ArgBest red[16];
     ArgBest b{-INFINITY, INT_MAX};
     for (int i = threadIdx.x; i < n; i += 1024) {
@@ -276,14 +277,16 @@ __global__ __launch_bounds__(1024) void k_argmax_first(const float * __restrict_
         ArgBest r = red[0];
         for (int w = 1; w < 16; ++w) r = arg_pick(r, red[w]);
         const bool nan0 = n > 0 && !(x[0] == x[0]);
-        out[0] = (nan0 || r.i == INT_MAX) ? 0 : r.i;
+        const int tok = (nan0 || r.i == INT_MAX) ? 0 : r.i;
+        out[0] = tok;
+        if (out2) out2[0] = tok;     // e.g. host-mapped memory: visible after the stream completes
     }
 }
 }  // namespace
 
-hipError_t launch_argmax(const float * x, int n, int * out, hipStream_t s) {
+hipError_t launch_argmax(const float * x, int n, int * out, hipStream_t s, int * out2) {
     if (n <= 0) return hipErrorInvalidValue;
-    LVK_LAUNCH(k_argmax_first, dim3(1), dim3(1024), 0, s, x, n, out);
+    LVK_LAUNCH(k_argmax_first, dim3(1), dim3(1024), 0, s, x, n, out, out2);
     return hipGetLastError();
 }
 }  // namespace lvk

@@ -10,8 +10,11 @@
 #include <cstdio>
 #include <cstring>
 #include <ctime>
+#include <csignal>
+#include <execinfo.h>
 #include <queue>
 #include <sys/mman.h>
+#include <unistd.h>
 
 #include "../../../include/llama.h"
 #include "../../../include/lvk_ops.h"
@@ -302,7 +305,31 @@ static int env_split_micro() {
     return e ? std::max(0, atoi(e)) : 64;
 }
 
+// LVK_SEGV_TRACE=1 (diagnostics): a SIGSEGV prints the faulting address and the native
+// frames to stderr, then the default action runs (core dump / exit 139)
+static void segv_trace(int sig, siginfo_t * si, void *) {
+    char buf[96];
+    const int n = snprintf(buf, sizeof(buf), "llama.vk_amd: signal %d at address %p; native frames:\n", sig,
+                           si ? si->si_addr : nullptr);
+    if (n > 0) (void) !write(2, buf, (size_t) n);
+    void * fr[64];
+    backtrace_symbols_fd(fr, backtrace(fr, 64), 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+static void maybe_install_segv_trace() {
+    static bool done = false;
+    if (done || !getenv("LVK_SEGV_TRACE")) return;
+    done = true;
+    struct sigaction sa {};
+    sa.sa_sigaction = segv_trace;
+    sa.sa_flags = SA_SIGINFO;
+    sigaction(SIGSEGV, &sa, nullptr);
+    sigaction(SIGBUS, &sa, nullptr);
+}
+
 struct llama_context * llama_init_from_file(const char * path_model, struct llama_context_params params) {
+    maybe_install_segv_trace();
     return init_context(path_model, params, 0, -1, env_split_devices(), getenv("LVK_SPLIT_TRANSPORT"),
                         env_split_micro());
 }

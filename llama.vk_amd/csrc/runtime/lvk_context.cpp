@@ -149,7 +149,9 @@ void Context::init(const llama_context_params & p) {
     *err_h = 0;
     LVK_HIP(hipHostGetDevicePointer((void **) &err_d, err_h, 0));
     greedy_d = (int *) model.alloc(4);
-    LVK_HIP(hipHostMalloc((void **) &greedy_h, 4, hipHostMallocDefault));
+    // the device argmax also stores the token straight into host-mapped memory
+    LVK_HIP(hipHostMalloc((void **) &greedy_h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    LVK_HIP(hipHostGetDevicePointer((void **) &greedy_hd, greedy_h, 0));
 
     // fp16 exp / silu tables (ggml.c:2915-2927), built with this host's glibc
     std::vector<uint16_t> te, ts;
@@ -423,8 +425,7 @@ void Context::build_graph(bool greedy) {
         LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
         enqueue_forward(1, true);
         if (greedy) {
-            LVK_HIP(launch_argmax(logits_d, (int) model.hp.n_vocab, greedy_d, stream));
-            LVK_HIP(hipMemcpyAsync(greedy_h, greedy_d, sizeof(int), hipMemcpyDeviceToHost, stream));
+            enqueue_argmax();
         } else if (model.has_head) {
             LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost,
                                    stream));
@@ -438,6 +439,12 @@ void Context::build_graph(bool greedy) {
     hipGraphExec_t & ge = greedy ? graph_greedy_exec : graph_exec;
     LVK_HIP(hipStreamEndCapture(stream, &g));
     LVK_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+}
+
+// greedy token of the last logits row: the device word feeds the stage link (lvk_split.cpp),
+// the host-mapped one the caller (read after the stream sync; no D2H copy node)
+void Context::enqueue_argmax() {
+    LVK_HIP(launch_argmax(logits_d, (int) model.hp.n_vocab, greedy_d, stream, greedy_hd));
 }
 
 // One decode step whose sampler is greedy, chosen on the device:
@@ -495,8 +502,7 @@ void Context::begin_eval(const int * tokens, int n, int n_past, const EvalPart &
                                    hipMemcpyHostToDevice, stream));
         enqueue_forward(n, last_only, tok_d + part.tok_off, last_only ? 0 : part.tok_off, part.head);
         if (part.greedy) {
-            LVK_HIP(launch_argmax(logits_d, V, greedy_d, stream));
-            LVK_HIP(hipMemcpyAsync(greedy_h, greedy_d, sizeof(int), hipMemcpyDeviceToHost, stream));
+            enqueue_argmax();
         } else if (model.has_head && part.copy_out) {
             LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost,
                                    stream));

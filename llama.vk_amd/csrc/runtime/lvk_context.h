@@ -128,7 +128,9 @@ struct Context {
     hipGraph_t graph_greedy = nullptr;
     hipGraphExec_t graph_greedy_exec = nullptr;
     int * greedy_d = nullptr;
-    int * greedy_h = nullptr;    // pinned
+    int * greedy_h = nullptr;    // host-mapped (coherent): the device argmax writes it
+    int * greedy_hd = nullptr;   // its device address
+    void enqueue_argmax();
 
     // host-visible results
     std::vector<float, PinnedAlloc<float>> logits;
