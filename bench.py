@@ -121,10 +121,10 @@ def cpu_info():
     return info
 
 
-def cpu_baseline(path, budget_s=20.0):
+def cpu_baseline(path, budget_s=20.0, label="7B Q4_0", prompt=True, seg_steps=16):
     """The reference AVX2 ggml.c build (oracle/_ref/libref.so) on the same file and tokens:
-    decode tok/s best of 3 segments and the 512-token prompt batch, llama.cpp:1186-1195's
-    n_eval / t_eval and n_p_eval / t_p_eval."""
+    decode tok/s best of 3 segments and (prompt=True) the 512-token prompt batch,
+    llama.cpp:1186-1195's n_eval / t_eval and n_p_eval / t_p_eval."""
     from oracle_lib import REF_SO, Ref
     if not os.path.exists(REF_SO):
         return None
@@ -139,7 +139,7 @@ def cpu_baseline(path, budget_s=20.0):
     toks = np.array(prompt_tokens(16), np.int32)
     lg = m.eval(toks, 0, n_threads=threads)
     tok, n_past = int(np.argmax(lg[-1])), 16
-    segs, seg_steps, t_used = [], 16, 0.0
+    segs, t_used = [], 0.0
     for _ in range(3):                                       # best of 3 decode segments
         t0 = time.perf_counter()
         for _ in range(seg_steps):
@@ -153,7 +153,7 @@ def cpu_baseline(path, budget_s=20.0):
             break
     p512 = np.array(prompt_tokens(512), np.int32)
     pr = []
-    for _ in range(3):                                       # 512-token prompt batch, best of up to 3
+    for _ in range(3 if prompt else 0):                      # 512-token prompt batch, best of up to 3
         t0 = time.perf_counter()
         m.eval(p512, 0, n_threads=threads)
         pr.append(512 / (time.perf_counter() - t0))
@@ -161,13 +161,17 @@ def cpu_baseline(path, budget_s=20.0):
         if t_used > budget_s:
             break
     m.close()
-    return {"value": max(segs), "unit": "tok/s", "cores": threads, "kind": "reference",
-            "sample": "reference ggml.c AVX2 build (oracle/_ref, compiled from the reference sources), the same "
-                      "synthetic 7B Q4_0 file and tokens, n_ctx 512, f16 KV, -t %d: 16-token prompt, then best of "
-                      "%d segments of %d greedy decode steps (positions 16..%d); prompt = one 512-token batch, "
-                      "best of %d" % (threads, len(segs), seg_steps, n_past - 1, len(pr)),
-            "decode_segments_tok_s": segs, "prompt_tok_s": max(pr), "prompt_runs_tok_s": pr,
-            "host": info}
+    out = {"value": max(segs), "unit": "tok/s", "cores": threads, "kind": "reference",
+           "sample": "reference ggml.c AVX2 build (oracle/_ref, compiled from the reference sources), the same "
+                     "synthetic %s file and tokens, n_ctx 512, f16 KV, -t %d: 16-token prompt, then best of "
+                     "%d segments of %d greedy decode steps (positions 16..%d)%s"
+                     % (label, threads, len(segs), seg_steps, n_past - 1,
+                        "; prompt = one 512-token batch, best of %d" % len(pr) if prompt else ""),
+           "decode_segments_tok_s": segs, "host": info}
+    if prompt:
+        out["prompt_tok_s"] = max(pr)
+        out["prompt_runs_tok_s"] = pr
+    return out
 
 
 SPLIT_TIMEOUT_S = 420
@@ -486,13 +490,27 @@ def main():
             lg = m13.eval([tok], 16 + (i % (n_ctx - 16)))
             tok = int(np.argmax(lg[-1]))
         t13 = all_max(pg, time.perf_counter() - t0)
+        # per-kernel-class HIP-event pass (the Q4_1 decode kernels, matvec_cu41.hip)
+        m13.set_profiling(True)
+        m13.reset_profile()
+        for i in range(16):
+            lg = m13.eval([tok], 16 + i * 31)
+            tok = int(np.argmax(lg[-1]))
+        p13 = m13.profile()
+        m13.set_profiling(False)
         m13.close()
+        k13 = {k: {"avg_us": v["ms"] / v["launches"] * 1e3,
+                   "gbs": v["bytes"] / v["launches"] / (v["ms"] / v["launches"] * 1e-3) / 1e9 if v["bytes"] else None}
+               for k, v in p13.items() if v["launches"]}
         r13 = args.steps_13b / t13
         q41 = {"value": n_gpus * r13, "unit": "tok/s", "steps": args.steps_13b,
                "workload": "LLaMA-13B Q4_1 (synthetic, seed 2) single-stream greedy decode, positions 16.., n_ctx 512",
                "model_bytes_per_token": MODEL_BYTES_13B_Q41,
                "frac_hbm_roofline": r13 * MODEL_BYTES_13B_Q41 / 1e9 / HBM_PEAK_GBS,
-               "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_13B_Q41}
+               "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_13B_Q41, "kernels": k13}
+        if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+            q41["cpu_baseline"] = cpu_baseline(path13, args.cpu_budget / 2, label="13B Q4_1", prompt=False,
+                                               seg_steps=8)
     # N > 1: LLaMA-65B split by layers over the ranks (RCCL send/recv of
     # the residual stream between stages)
     split = None
