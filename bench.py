@@ -411,6 +411,26 @@ def main():
         for _ in range(200):
             m.sample(last64, 40, 0.95, 0.8, 1.1)
         greedy["host_sampler_us"] = (time.perf_counter() - t0) / 200 * 1e6
+        # sampled decode at main's defaults: llama_eval + the host sampler over all logits,
+        # against lvk_eval_sample (repeat penalty, temperature and top-k on the device, the
+        # host finishing over the 40 candidates)
+        rates = {}
+        for mode in ("host", "device"):
+            m.eval(ptoks, 0)
+            win = list(prompt_tokens(64))
+            tok = m.sample(np.array(win, np.int32), 40, 0.95, 0.8, 1.1)
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                win = win[1:] + [tok]
+                pos = 16 + (i % (n_ctx - 16))
+                if mode == "host":
+                    m.eval([tok], pos)
+                    tok = m.sample(np.array(win, np.int32), 40, 0.95, 0.8, 1.1)
+                else:
+                    tok = m.eval_sample(tok, pos, np.array(win, np.int32), 40, 0.95, 0.8, 1.1)
+            rates[mode] = args.steps / (time.perf_counter() - t0)
+        greedy["sampled_decode_tok_s"] = {"host_sampler": rates["host"], "device_sampler": rates["device"],
+                                          "settings": "top_k 40, top_p 0.95, temp 0.8, repeat_penalty 1.1 over 64"}
 
     # prompt eval: one 512-token batch (configs[2])
     p512 = np.array(prompt_tokens(512), np.int32)

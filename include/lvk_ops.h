@@ -119,6 +119,25 @@ LVK_API int lvk_decode_persistent_active(struct llama_context * ctx);
  * lvk_argmax(x, n) is the op-level kernel on a host array: the first index whose
  * value is strictly greater than all earlier ones (0 when x[0] is NaN). */
 LVK_API int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past);
+/* On-device sampling: lvk_eval_sample(ctx, token, n_past, last_n, n_last,
+ * top_k, top_p, temp, repeat_penalty) returns what llama_eval(ctx, &token, 1, n_past, .)
+ * followed by llama_sample_top_p_top_k(ctx, last_n, n_last, top_k, top_p, temp,
+ * repeat_penalty) returns (llama.cpp:1356-1459, 1703-1719, 1777-1805), drawing from the same
+ * mt19937 stream.  The repeat penalty, the temperature and the top-k selection run over the
+ * logits in HBM (sample.hip); only the candidates >= the k-th value cross PCIe and the host
+ * finishes the reference's softmax / top-p / discrete_distribution over k values.  Ties among
+ * the candidates, NaN logits, top_k <= 0 or > 1024, a last-n window > 1024, split or
+ * logits_all contexts take the reference path over all logits (same result, slower).
+ * temp <= 0 is lvk_eval_greedy.  The host logits of llama_get_logits are NOT refreshed
+ * (except on the all-logits path).  Returns the token, or -1 on error. */
+/* op-level device candidate selection on a host array (sample.hip): the values the reference
+ * sorts (x[i] / temp, with the repeat penalty for ids in last[]), every one >= the k-th largest
+ * written to vals/ids (arbitrary order, up to 1024), *flags bit 1 = NaN seen, bit 2 = more than
+ * 1024 candidates.  Returns the candidate count, -1 on bad arguments. */
+LVK_API int lvk_sample_candidates(const float * x, int n, const int * last, int n_last, int k, float temp, float rp,
+                                  float * vals, int * ids, int * flags);
+LVK_API int lvk_eval_sample(struct llama_context * ctx, int token, int n_past, const int * last_n, int n_last,
+                            int top_k, float top_p, float temp, float repeat_penalty);
 LVK_API int lvk_argmax(const float * x, int n);
 
 /* Device-side KV state (the host-bytes form is llama_get_kv_cache /

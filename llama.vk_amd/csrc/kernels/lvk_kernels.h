@@ -260,6 +260,29 @@ hipError_t launch_decode_persistent(const DecodeArgs & A, const DecodeArgs * A_d
 }  // namespace lvk
 
 namespace lvk {
+// device half of llama_sample_top_p_top_k (sample.hip): repeat penalty + temperature on the
+// logits in HBM, radix select of the k-th largest value, every value >= it written to out
+// (host-mapped).  SampleParams lives in device memory (one H2D copy per step).
+constexpr int SAMPLE_MAX_VOCAB = 32768;   // values per thread kept in registers
+constexpr int SAMPLE_CAP = 1024;          // candidates the host can receive (k <= this)
+constexpr int SAMPLE_MAX_LAST = 1024;     // last-n window entries
+enum SampleFlags : int { SAMPLE_FLAG_NAN = 1, SAMPLE_FLAG_OVERFLOW = 2 };
+struct SampleParams {
+    int k;                    // top_k (1..SAMPLE_CAP)
+    int n_last;               // entries of last[]
+    float scale;              // 1.0f / temp
+    float rp;                 // repeat_penalty
+    int last[SAMPLE_MAX_LAST];
+};
+struct SampleOut {
+    int count;                // candidates (values >= the k-th largest)
+    int flags;                // SampleFlags
+    int pad[2];
+    float val[SAMPLE_CAP];
+    int id[SAMPLE_CAP];
+};
+hipError_t launch_sample_cand(const float * logits, int n, const SampleParams * P, SampleOut * out, hipStream_t s);
+
 // y[t] = g * rms_norm(x[t]) as f32 (the embeddings output, llama.cpp:1117-1124)
 hipError_t launch_rmsnorm_rows(const float * x, const float * g, int K, int n, float * y, hipStream_t s);
 // greedy argmax over x[0..n) with the reference's first-maximum rule (llama.cpp:1382-1394); *out on the device

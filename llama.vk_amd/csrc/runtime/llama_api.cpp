@@ -6,6 +6,7 @@
 // valid until the next eval, no thread safety.  Tokenizer and sampler are host
 // code with the reference's exact tie-breaking (same std::priority_queue /
 // std::partial_sort / std::discrete_distribution over std::mt19937).
+#include <algorithm>
 #include <cinttypes>
 #include <cstdio>
 #include <cstring>
@@ -94,6 +95,8 @@ std::vector<int> tokenize(const lvk::Vocab & vocab, const std::string & text, bo
 // ---------------------------------------------------------------------------
 // sampler (llama.cpp:1352-1459)
 // ---------------------------------------------------------------------------
+int sample_from_top_k(lvk::Context & c, std::vector<std::pair<float, int>> & cand, float top_p);
+
 int sample_top_p_top_k(lvk::Context & c, const std::vector<int> & last, int top_k, float top_p, float temp,
                        float repeat_penalty) {
     const int n_logits = (int) c.model.hp.n_vocab;
@@ -131,6 +134,13 @@ int sample_top_p_top_k(lvk::Context & c, const std::vector<int> & last, int top_
     std::partial_sort(cand.begin(), cand.begin() + k, cand.end(),
                       [](const std::pair<float, int> & a, const std::pair<float, int> & b) { return a.first > b.first; });
     cand.resize(k);
+    return sample_from_top_k(c, cand, top_p);
+}
+
+// the reference's sampler after sample_top_k (llama.cpp:1419-1456): softmax over the k
+// candidates in descending order (expf, double sum), the top-p cut, std::discrete_distribution
+// over the context's mt19937
+int sample_from_top_k(lvk::Context & c, std::vector<std::pair<float, int>> & cand, float top_p) {
     std::vector<float> probs;
     probs.reserve(cand.size());
     const float maxl = cand[0].first;
@@ -493,6 +503,72 @@ llama_token llama_sample_top_p_top_k(struct llama_context * ctx, const llama_tok
     const int64_t t0 = lvk::now_us();
     const std::vector<int> last(last_n_tokens_data, last_n_tokens_data + last_n_tokens_size);
     const int r = sample_top_p_top_k(c, last, top_k, top_p, temp, repeat_penalty);
+    c.t_sample_us += lvk::now_us() - t0;
+    c.n_sample++;
+    return r;
+}
+
+// lvk_eval_sample (include/lvk_ops.h): llama_eval of one token + llama_sample_top_p_top_k,
+// the O(n_vocab) part of the sampler on the device (sample.hip)
+int lvk_eval_sample(struct llama_context * ctx, int token, int n_past, const int * last_n, int n_last, int top_k,
+                    float top_p, float temp, float repeat_penalty) {
+    lvk::Context & c = ctx->c;
+    if (temp <= 0) return lvk_eval_greedy(ctx, token, n_past);   // llama.cpp:1382-1394
+    if (n_last < 0 || (n_last > 0 && !last_n)) {
+        fprintf(stderr, "%s: bad last-n window\n", __func__);
+        return -1;
+    }
+    const int n_vocab = (int) c.model.hp.n_vocab;
+    const int k = top_k > 0 ? std::min(top_k, n_vocab) : n_vocab;
+    auto host_path = [&]() -> int {
+        if (llama_eval(ctx, &token, 1, n_past, 1) != 0) return -1;
+        return llama_sample_top_p_top_k(ctx, last_n, n_last, top_k, top_p, temp, repeat_penalty);
+    };
+    if (ctx->split || c.logits_all || k > lvk::SAMPLE_CAP || n_last > lvk::SAMPLE_MAX_LAST || n_vocab > lvk::SAMPLE_MAX_VOCAB)
+        return host_path();
+    int64_t t0 = lvk::now_us();
+    lvk::SampleParams & sp = *c.samp_h;
+    sp.k = k;
+    sp.n_last = n_last;
+    sp.scale = 1.0f / temp;            // llama.cpp:1398
+    sp.rp = repeat_penalty;
+    if (n_last > 0) std::memcpy(sp.last, last_n, sizeof(int) * (size_t) n_last);
+    try {
+        c.eval_sample(token, n_past);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: failed to eval: %s\n", __func__, e.msg.c_str());
+        return -1;
+    }
+    c.t_eval_us += lvk::now_us() - t0;
+    c.n_eval++;
+    t0 = lvk::now_us();
+    const lvk::SampleOut & so = *c.sout_h;
+    std::vector<std::pair<float, int>> cand;
+    bool exact = so.flags == 0 && so.count >= k && so.count <= lvk::SAMPLE_CAP;
+    if (exact) {
+        cand.reserve((size_t) so.count);
+        for (int i = 0; i < so.count; ++i) cand.emplace_back(so.val[i], so.id[i]);
+        std::sort(cand.begin(), cand.end(),
+                  [](const std::pair<float, int> & a, const std::pair<float, int> & b) { return a.first > b.first; });
+        // distinct values: the descending order is the one std::partial_sort leaves; a tie
+        // anywhere among the candidates (their order is the heap's) takes the reference path
+        for (size_t i = 1; i < cand.size() && exact; ++i) exact = cand[i - 1].first != cand[i].first;
+    }
+    int r;
+    if (exact) {
+        cand.resize((size_t) k);
+        r = sample_from_top_k(c, cand, top_p);
+    } else {
+        try {
+            c.fetch_logits();
+        } catch (const lvk::Error & e) {
+            fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());
+            return -1;
+        }
+        const std::vector<int> last(last_n, last_n + n_last);
+        r = sample_top_p_top_k(c, last, top_k, top_p, temp, repeat_penalty);
+        c.n_sample_fallback++;
+    }
     c.t_sample_us += lvk::now_us() - t0;
     c.n_sample++;
     return r;

@@ -64,6 +64,10 @@ Context::~Context() {
     if (graph) (void) hipGraphDestroy(graph);
     if (graph_greedy_exec) (void) hipGraphExecDestroy(graph_greedy_exec);
     if (graph_greedy) (void) hipGraphDestroy(graph_greedy);
+    if (graph_sample_exec) (void) hipGraphExecDestroy(graph_sample_exec);
+    if (graph_sample) (void) hipGraphDestroy(graph_sample);
+    if (samp_h) (void) hipHostFree(samp_h);
+    if (sout_h) (void) hipHostFree(sout_h);
     if (greedy_h) (void) hipHostFree(greedy_h);
     for (auto & e : ev_pool) { (void) hipEventDestroy(e.first); (void) hipEventDestroy(e.second); }
     if (sp_h) (void) hipHostFree(sp_h);
@@ -152,6 +156,11 @@ void Context::init(const llama_context_params & p) {
     // the device argmax also stores the token straight into host-mapped memory
     LVK_HIP(hipHostMalloc((void **) &greedy_h, 64, hipHostMallocMapped | hipHostMallocCoherent));
     LVK_HIP(hipHostGetDevicePointer((void **) &greedy_hd, greedy_h, 0));
+    samp_d = (SampleParams *) model.alloc(sizeof(SampleParams));
+    LVK_HIP(hipHostMalloc((void **) &samp_h, sizeof(SampleParams), hipHostMallocDefault));
+    std::memset(samp_h, 0, sizeof(SampleParams));
+    LVK_HIP(hipHostMalloc((void **) &sout_h, sizeof(SampleOut), hipHostMallocMapped | hipHostMallocCoherent));
+    LVK_HIP(hipHostGetDevicePointer((void **) &sout_d, sout_h, 0));
 
     // fp16 exp / silu tables (ggml.c:2915-2927), built with this host's glibc
     std::vector<uint16_t> te, ts;
@@ -254,6 +263,8 @@ void Context::set_decode_persistent(bool on) {
     if (graph) { (void) hipGraphDestroy(graph); graph = nullptr; }
     if (graph_greedy_exec) { (void) hipGraphExecDestroy(graph_greedy_exec); graph_greedy_exec = nullptr; }
     if (graph_greedy) { (void) hipGraphDestroy(graph_greedy); graph_greedy = nullptr; }
+    if (graph_sample_exec) { (void) hipGraphExecDestroy(graph_sample_exec); graph_sample_exec = nullptr; }
+    if (graph_sample) { (void) hipGraphDestroy(graph_sample); graph_sample = nullptr; }
 }
 
 static double qbytes(const QMatrix & w) { return (double) w.M * (w.K / 32) * (w.qtype == Q4_0 ? 20 : 24); }
@@ -416,16 +427,20 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
         LVK_HIP(launch_rmsnorm_rows(x + (size_t) (n - 1) * E, model.norm, E, 1, emb_d, stream));
 }
 
-void Context::build_graph(bool greedy) {
+void Context::build_graph(int kind) {
     // one replay per token: the step block H2D, the forward pass and the logits D2H
     // (both host buffers page-locked, the logits one sized before the capture); the
-    // greedy variant ends in the device argmax and copies back 4 bytes instead
+    // greedy variant ends in the device argmax (token into host-mapped memory), the sample
+    // variant copies the sampler block in and ends in the device top-k candidates
     LVK_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
         LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
+        if (kind == 2) LVK_HIP(hipMemcpyAsync(samp_d, samp_h, sizeof(SampleParams), hipMemcpyHostToDevice, stream));
         enqueue_forward(1, true);
-        if (greedy) {
+        if (kind == 1) {
             enqueue_argmax();
+        } else if (kind == 2) {
+            LVK_HIP(launch_sample_cand(logits_d, (int) model.hp.n_vocab, samp_d, sout_d, stream));
         } else if (model.has_head) {
             LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost,
                                    stream));
@@ -435,8 +450,8 @@ void Context::build_graph(bool greedy) {
         (void) hipStreamEndCapture(stream, &g);
         throw;
     }
-    hipGraph_t & g = greedy ? graph_greedy : graph;
-    hipGraphExec_t & ge = greedy ? graph_greedy_exec : graph_exec;
+    hipGraph_t & g = kind == 1 ? graph_greedy : kind == 2 ? graph_sample : graph;
+    hipGraphExec_t & ge = kind == 1 ? graph_greedy_exec : kind == 2 ? graph_sample_exec : graph_exec;
     LVK_HIP(hipStreamEndCapture(stream, &g));
     LVK_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
 }
@@ -460,6 +475,26 @@ int Context::eval_greedy(int token, int n_past) {
     return *greedy_h;
 }
 
+// One decode step whose sampler runs its O(n_vocab) part on the device:
+// the forward pass of eval(&token, 1, n_past), then sample.hip's repeat penalty, temperature
+// and top-k candidates over the logits in HBM (parameters in *samp_h).  Host logits are not
+// refreshed (llama_get_logits keeps the previous eval's).
+void Context::eval_sample(int token, int n_past) {
+    if (!model.has_head || !model.has_embed) throw Error("llama.vk_amd: sampling eval needs the whole model");
+    if ((int) model.hp.n_vocab > SAMPLE_MAX_VOCAB) throw Error("llama.vk_amd: vocabulary too large for the device sampler");
+    EvalPart part;
+    part.sample = true;
+    begin_eval(&token, 1, n_past, part);
+    end_eval(true);
+}
+
+void Context::fetch_logits() {
+    const size_t V = model.hp.n_vocab;
+    logits.resize(V);
+    LVK_HIP(hipMemcpy(logits.data(), logits_d, V * sizeof(float), hipMemcpyDeviceToHost));
+    logits_valid = true;
+}
+
 void Context::eval(const int * tokens, int n, int n_past) {
     begin_eval(tokens, n, n_past, EvalPart{});
     end_eval(false);
@@ -471,8 +506,8 @@ void Context::begin_eval(const int * tokens, int n, int n_past, const EvalPart &
     const int n_total = part.n_total < 0 ? n : part.n_total;
     if (n <= 0 || n_past < 0 || n_past + n > n_ctx || part.tok_off < 0 || part.tok_off + n > n_total)
         throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
-    if (part.greedy && (!model.has_head || n != 1 || logits_all))
-        throw Error("llama.vk_amd: greedy eval needs the lm_head stage, one token and last-token logits");
+    if ((part.greedy || part.sample) && (!model.has_head || n != 1 || logits_all))
+        throw Error("llama.vk_amd: greedy / sampling eval needs the lm_head stage, one token and last-token logits");
     if (model.has_embed) {
         if (!tokens) throw Error("llama.vk_amd: the first stage needs tokens");
         for (int i = 0; i < n; ++i)
@@ -492,35 +527,39 @@ void Context::begin_eval(const int * tokens, int n, int n_past, const EvalPart &
     if (model.has_head && part.tok_off == 0)   // within the reserve: the pointer never moves
         logits.resize((size_t) (last_only ? 1 : n_total) * V);
     if (graph_ok) {
-        hipGraphExec_t & ge = part.greedy ? graph_greedy_exec : graph_exec;
-        if (!ge) build_graph(part.greedy);
+        const int kind = part.greedy ? 1 : part.sample ? 2 : 0;
+        hipGraphExec_t & ge = kind == 1 ? graph_greedy_exec : kind == 2 ? graph_sample_exec : graph_exec;
+        if (!ge) build_graph(kind);
         LVK_HIP(hipGraphLaunch(ge, stream));
     } else {
         LVK_HIP(hipMemcpyAsync(sp_d, sh, sizeof(StepParams), hipMemcpyHostToDevice, stream));
+        if (part.sample) LVK_HIP(hipMemcpyAsync(samp_d, samp_h, sizeof(SampleParams), hipMemcpyHostToDevice, stream));
         if (n > 1)
             LVK_HIP(hipMemcpyAsync(tok_d + part.tok_off, tok_h + part.tok_off, sizeof(int) * (size_t) n,
                                    hipMemcpyHostToDevice, stream));
         enqueue_forward(n, last_only, tok_d + part.tok_off, last_only ? 0 : part.tok_off, part.head);
         if (part.greedy) {
             enqueue_argmax();
+        } else if (part.sample) {
+            LVK_HIP(launch_sample_cand(logits_d, V, samp_d, sout_d, stream));
         } else if (model.has_head && part.copy_out) {
             LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost,
                                    stream));
         }
     }
-    if (want_embedding && model.has_head && part.copy_out && !part.greedy) {
+    if (want_embedding && model.has_head && part.copy_out && !part.greedy && !part.sample) {
         embedding.resize(hp.n_embd);
         LVK_HIP(hipMemcpyAsync(embedding.data(), emb_d, sizeof(float) * hp.n_embd, hipMemcpyDeviceToHost, stream));
     }
 }
 
-void Context::end_eval(bool greedy) {
+void Context::end_eval(bool no_host_logits) {
     sp_next = 1;
     LVK_HIP(hipStreamSynchronize(stream));
     if (profiling) collect_profile();
     check_device_error();
     // after lvk_eval_greedy llama_get_logits still holds an earlier eval's row
-    logits_valid = model.has_head && !greedy;
+    logits_valid = model.has_head && !no_host_logits;
 }
 
 size_t Context::kv_bytes() const {

@@ -55,6 +55,7 @@ struct EvalPart {
     bool head = true;     // run norm + lm_head (last stage: the call's last slice, or logits_all)
     bool copy_out = true; // copy logits / embedding / the greedy token to the host after this slice
     bool greedy = false;  // end in the device argmax (lvk_eval_greedy) instead of the logits D2H
+    bool sample = false;  // end in the device top-k candidates (lvk_eval_sample) instead of the logits D2H
 };
 
 struct Context {
@@ -127,6 +128,20 @@ struct Context {
     // greedy decode graph (lvk_eval_greedy): argmax on the device, 4-byte D2H instead of the logits row
     hipGraph_t graph_greedy = nullptr;
     hipGraphExec_t graph_greedy_exec = nullptr;
+    // sampling decode graph (lvk_eval_sample): the sampler block H2D, the forward pass and the
+    // device top-k candidates (sample.hip) into host-mapped memory instead of the logits row
+    hipGraph_t graph_sample = nullptr;
+    hipGraphExec_t graph_sample_exec = nullptr;
+    SampleParams * samp_h = nullptr;   // pinned host block, filled per call
+    SampleParams * samp_d = nullptr;
+    SampleOut * sout_h = nullptr;      // host-mapped candidates
+    SampleOut * sout_d = nullptr;      // its device address
+    // one single-token eval + the device half of the sampler (samp_h filled by the caller);
+    // the candidates are in *sout_h afterwards
+    void eval_sample(int token, int n_past);
+    // the last eval's last-token logits row -> host logits (llama_get_logits valid again)
+    void fetch_logits();
+    int n_sample_fallback = 0;         // lvk_eval_sample calls that took the all-logits host path
     int * greedy_d = nullptr;
     int * greedy_h = nullptr;    // host-mapped (coherent): the device argmax writes it
     int * greedy_hd = nullptr;   // its device address
@@ -159,12 +174,12 @@ struct Context {
     // profile, device error word); a layer split interleaves the stages' begin_evals
     // with the residual-stream hand-offs and ends them together
     void begin_eval(const int * tokens, int n, int n_past, const EvalPart & part);
-    void end_eval(bool greedy);
+    void end_eval(bool no_host_logits);
     // stage boundary: copy the residual stream x [n][E] to (to_ctx) or from the context
     void x_copy(void * buf, int n, bool to_ctx, bool on_device);
     void enqueue_forward(int n, bool last_only, const int * tok_src = nullptr, int logit_row = 0, bool head = true);
     bool use_mfma(int n) const;
-    void build_graph(bool greedy = false);
+    void build_graph(int kind = 0);      // 0 logits, 1 greedy, 2 sample
     int eval_greedy(int token, int n_past);
     void kv_get();
     void kv_set(const uint8_t * src, size_t n);

@@ -339,6 +339,34 @@ int lvk_argmax(const float * x, int n) {
     } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
 }
 
+int lvk_sample_candidates(const float * x, int n, const int * last, int n_last, int k, float temp, float rp,
+                          float * vals, int * ids, int * flags) {
+    try {
+        if (n <= 0 || n > lvk::SAMPLE_MAX_VOCAB || k < 1 || k > std::min(n, lvk::SAMPLE_CAP) || temp <= 0 ||
+            n_last < 0 || n_last > lvk::SAMPLE_MAX_LAST || (n_last > 0 && !last))
+            throw lvk::Error("arguments out of range");
+        Dev dv;
+        float * xd = dv.up(x, (size_t) n);
+        lvk::SampleParams p{};
+        p.k = k;
+        p.n_last = n_last;
+        p.scale = 1.0f / temp;
+        p.rp = rp;
+        if (n_last > 0) std::memcpy(p.last, last, sizeof(int) * (size_t) n_last);
+        auto * pd = (lvk::SampleParams *) dv.get(sizeof(p));
+        LVK_HIP(hipMemcpy(pd, &p, sizeof(p), hipMemcpyHostToDevice));
+        auto * od = (lvk::SampleOut *) dv.get(sizeof(lvk::SampleOut));
+        LVK_HIP(lvk::launch_sample_cand(xd, n, pd, od, nullptr));
+        lvk::SampleOut o;
+        LVK_HIP(hipMemcpy(&o, od, sizeof(o), hipMemcpyDeviceToHost));
+        const int m = std::min(o.count, lvk::SAMPLE_CAP);
+        std::memcpy(vals, o.val, sizeof(float) * (size_t) m);
+        std::memcpy(ids, o.id, sizeof(int) * (size_t) m);
+        *flags = o.flags;
+        return o.count;
+    } catch (const lvk::Error & e) { return fail(__func__, e.msg); }
+}
+
 int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past) {
     lvk::Context & c = ctx->c;
     const int64_t t0 = lvk::now_us();

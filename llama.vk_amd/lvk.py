@@ -74,6 +74,7 @@ _sig("llama_get_embeddings", C.POINTER(C.c_float), [C.c_void_p])
 _sig("llama_token_to_str", C.c_char_p, [C.c_void_p, C.c_int])
 _sig("llama_token_bos", C.c_int, [])
 _sig("llama_token_eos", C.c_int, [])
+_sig("lvk_eval_sample", C.c_int, [C.c_void_p, C.c_int, C.c_int, i32p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float])
 _sig("llama_sample_top_p_top_k", C.c_int, [C.c_void_p, i32p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float])
 _sig("llama_print_timings", None, [C.c_void_p])
 _sig("llama_reset_timings", None, [C.c_void_p])
@@ -103,6 +104,7 @@ _sig("lvk_decode_persistent_active", C.c_int, [C.c_void_p])
 _sig("lvk_set_prompt_exact", None, [C.c_void_p, C.c_int])
 _sig("lvk_eval_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_argmax", C.c_int, [f32p, C.c_int])
+_sig("lvk_sample_candidates", C.c_int, [f32p, C.c_int, i32p, C.c_int, C.c_int, C.c_float, C.c_float, f32p, i32p, C.POINTER(C.c_int)])
 _sig("lvk_kv_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_int])
 _sig("lvk_init_stage", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, C.c_int])
 _sig("lvk_stage_eval", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
@@ -239,6 +241,14 @@ class Llama:
 
     def token_to_str(self, tok):
         return lib.llama_token_to_str(self.ctx, tok)
+
+    def eval_sample(self, token, n_past, last_tokens, top_k=40, top_p=0.95, temp=0.8, repeat_penalty=1.1):
+        """lvk_eval_sample: one decode step + the sampler with its O(n_vocab) part on the GPU"""
+        lt = np.ascontiguousarray(last_tokens, dtype=np.int32)
+        r = lib.lvk_eval_sample(self.ctx, int(token), int(n_past), lt, len(lt), top_k, top_p, temp, repeat_penalty)
+        if r < 0:
+            raise RuntimeError("lvk_eval_sample failed")
+        return r
 
     def sample(self, last_tokens, top_k=40, top_p=0.95, temp=0.8, repeat_penalty=1.1):
         lt = np.ascontiguousarray(last_tokens, np.int32)
@@ -392,6 +402,20 @@ def argmax(x):
     if r < 0:
         raise RuntimeError("lvk_argmax failed")
     return r
+
+
+def sample_candidates(x, last, k, temp, rp):
+    """lvk_sample_candidates: (values, ids, flags) of the device top-k candidate selection"""
+    x = np.ascontiguousarray(x, np.float32)
+    last = np.ascontiguousarray(last, np.int32)
+    vals = np.zeros(1024, np.float32)
+    ids = np.zeros(1024, np.int32)
+    fl = C.c_int(0)
+    n = lib.lvk_sample_candidates(x, x.size, last, last.size, k, temp, rp, vals, ids, C.byref(fl))
+    if n < 0:
+        raise RuntimeError("lvk_sample_candidates failed")
+    m = min(n, 1024)
+    return vals[:m], ids[:m], fl.value, n
 
 
 def rms_norm_mul(x, g):
