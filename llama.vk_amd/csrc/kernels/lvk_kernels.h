@@ -202,6 +202,8 @@ hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 
 
 // operator-level helpers used by the C ABI tests
 hipError_t launch_quantize_act(const float * x, int N, int K, int qtype, ActQ out, hipStream_t s);
+// the reference's scalar quantize_row_q4_0/1_reference (roundf, id = 1/d)
+hipError_t launch_quantize_ref(const float * x, int N, int K, int qtype, ActQ out, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Persistent single-token decode (decode_persistent.hip): the whole forward pass of

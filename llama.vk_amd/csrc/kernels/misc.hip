@@ -172,7 +172,54 @@ __global__ void k_quantize_q40(const float * __restrict__ x, int N, int K, ActQ 
     out.qs[(size_t) t * out.nb + b] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// the reference's scalar quantizers (quantize_row_q4_0_reference / _q4_1_reference,
+// ggml.c:509-545 / 799-840): roundf (half away from zero) and id = 1/d, unlike the AVX2
+// quantizers above (RNE, id = 7/amax); one thread per block, output split like ActQ
+__global__ void k_quantize_ref(const float * __restrict__ x, int N, int K, int qtype, ActQ out) {
+    const int nb = K / 32;
+    const long idx = (long) blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long) N * nb) return;
+    const int t = (int) (idx / nb), b = (int) (idx % nb);
+    const float * xb = x + (size_t) t * K + (size_t) b * 32;
+    uint32_t w[4] = {0, 0, 0, 0};
+    float d, mn = 0.0f;
+    if (qtype == Q4_0) {
+        float amax = 0.0f;
+        for (int l = 0; l < 32; ++l) { const float a = fabsf(xb[l]); amax = amax > a ? amax : a; }   // MAX(amax, |v|)
+        d = amax / 7.0f;
+        const float id = d != 0.0f ? 1.0f / d : 0.0f;
+        for (int l = 0; l < 32; ++l) {
+            const uint32_t q = (uint32_t) (uint8_t) ((int8_t) roundf(xb[l] * id) + 8);
+            w[l / 8] |= (q & 0xFFu) << (4 * (l % 8));
+        }
+    } else {
+        float mx = -3.402823466e+38f;
+        mn = 3.402823466e+38f;
+        for (int l = 0; l < 32; ++l) {
+            const float v = xb[l];
+            if (v < mn) mn = v;
+            if (v > mx) mx = v;
+        }
+        d = (mx - mn) / 15.0f;
+        const float id = d != 0.0f ? 1.0f / d : 0.0f;
+        for (int l = 0; l < 32; ++l) {
+            const uint32_t q = (uint32_t) (uint8_t) roundf((xb[l] - mn) * id);
+            w[l / 8] |= (q & 0xFFu) << (4 * (l % 8));
+        }
+    }
+    out.d[(size_t) t * out.nb + b] = d;
+    if (qtype == Q4_1) out.m[(size_t) t * out.nb + b] = mn;
+    out.qs[(size_t) t * out.nb + b] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 }  // namespace
+
+hipError_t launch_quantize_ref(const float * x, int N, int K, int qtype, ActQ out, hipStream_t s) {
+    if (K % 32 || (qtype != Q4_0 && qtype != Q4_1)) return hipErrorInvalidValue;
+    const long n = (long) N * (K / 32);
+    hipLaunchKernelGGL(k_quantize_ref, dim3((unsigned) ((n + 127) / 128)), dim3(128), 0, s, x, N, K, qtype, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_embed(const void * emb, int emb_type, int n_embd, const int * tokens, int n, float * x,
                         hipStream_t s) {

@@ -404,6 +404,50 @@ def argmax(x):
     return r
 
 
+class _QuantizeFns(C.Structure):      # quantize_fns_t (include/ggml.h, reference ggml.h:808-813)
+    _fields_ = [("dequantize_row_q", C.c_void_p), ("quantize_row_q", C.c_void_p),
+                ("quantize_row_q_reference", C.c_void_p), ("vec_dot_q", C.c_void_p)]
+
+
+_DEQ_T = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int)
+_Q_T = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int)
+_DOT_T = C.CFUNCTYPE(None, C.c_int, C.POINTER(C.c_float), C.c_void_p, C.c_void_p)
+_sig("ggml_internal_get_quantize_fn", _QuantizeFns, [C.c_size_t])
+
+
+class QuantizeFns:
+    """ggml_internal_get_quantize_fn(ggml_type) as Python callables (numpy in and out)"""
+
+    def __init__(self, ggml_type):
+        t = lib.ggml_internal_get_quantize_fn(ggml_type)
+        self.valid = bool(t.vec_dot_q)
+        self.bb = 20 if ggml_type == 0 else 24
+        if self.valid:
+            self._deq = _DEQ_T(t.dequantize_row_q)
+            self._q = _Q_T(t.quantize_row_q)
+            self._qr = _Q_T(t.quantize_row_q_reference)
+            self._dot = _DOT_T(t.vec_dot_q)
+
+    def quantize_row(self, x, reference=False):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.zeros(x.size // 32 * self.bb, np.uint8)
+        (self._qr if reference else self._q)(x.ctypes.data, y.ctypes.data, x.size)
+        return y
+
+    def dequantize_row(self, q, k):
+        q = np.ascontiguousarray(q, np.uint8)
+        y = np.zeros(k, np.float32)
+        self._deq(q.ctypes.data, y.ctypes.data, k)
+        return y
+
+    def vec_dot(self, n, x, y):
+        x = np.ascontiguousarray(x, np.uint8)
+        y = np.ascontiguousarray(y, np.uint8)
+        s = C.c_float(0.0)
+        self._dot(n, C.byref(s), x.ctypes.data, y.ctypes.data)
+        return s.value
+
+
 def sample_candidates(x, last, k, temp, rp):
     """lvk_sample_candidates: (values, ids, flags) of the device top-k candidate selection"""
     x = np.ascontiguousarray(x, np.float32)

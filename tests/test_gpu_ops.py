@@ -206,3 +206,45 @@ def test_mul_mat_mfma_bit_exact(lvk, oracle, m, k, n, norm):
         xin = (g[None, :] * xn).astype(np.float32)
     want = _oracle_mm(oracle, wq, [oracle.quantize(r, 2) for r in xin], k, 2)
     assert np.array_equal(bits(got), bits(want))
+
+
+# ---------------------------------------------------------------------------
+# the reference's op-level codec table (ggml.h:803-814) exported by this library
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("qt,k", [(2, 256), (2, 4096), (2, 96), (3, 5120), (3, 4096), (3, 160)])
+def test_ggml_internal_get_quantize_fn_vs_oracle(lvk, oracle, qt, k):
+    """ggml_internal_get_quantize_fn(GGML_TYPE_Q4_0 / _Q4_1): quantize_row_q (AVX2 rules),
+    quantize_row_q_reference (roundf), dequantize_row_q and vec_dot_q, each on the GPU, bit-exact
+    against the oracle's restatement of the same reference functions (k not a multiple of 256
+    exercises the zero-block padding of vec_dot_q)"""
+    f = lvk.QuantizeFns(0 if qt == 2 else 1)
+    assert f.valid
+    rng = np.random.default_rng(qt * 1000 + k)
+    x = (rng.standard_normal(k) * 1.7).astype(np.float32)
+    x[:32] = 0.0                                   # an all-zero block
+    if k >= 96:
+        x[64:96] = np.float32(2.5) * (np.arange(32) % 2 * 2 - 1)   # ties at the rounding boundary
+    for ref in (False, True):
+        got = f.quantize_row(x, reference=ref)
+        assert np.array_equal(got, oracle.quantize(x, qt, reference=ref)), "reference=%s" % ref
+    q = oracle.quantize(x, qt)
+    assert np.array_equal(f.dequantize_row(q, k).view(np.uint32), oracle.dequantize(q, qt, k).view(np.uint32))
+    w = oracle.quantize((rng.standard_normal(k) * 0.6).astype(np.float32), qt)
+    got = np.float32(f.vec_dot(k, w, q))
+    want = np.float32(oracle.vec_dot(qt, k, w, q))
+    assert got.view(np.uint32) == want.view(np.uint32)
+
+
+def test_ggml_internal_get_quantize_fn_vs_reference_build(lvk, ref):
+    """the same four functions against the reference build's own table (oracle/_ref/libref.so)"""
+    for qt in (2, 3):
+        f = lvk.QuantizeFns(0 if qt == 2 else 1)
+        rng = np.random.default_rng(qt)
+        x = (rng.standard_normal(4096) * 2.2).astype(np.float32)
+        for reff in (False, True):
+            assert np.array_equal(f.quantize_row(x, reference=reff), ref.quantize(x, qt, reference=reff))
+        q = ref.quantize(x, qt)
+        assert np.array_equal(f.dequantize_row(q, 4096).view(np.uint32), ref.dequantize(q, qt, 4096).view(np.uint32))
+        w = ref.quantize((rng.standard_normal(4096) * 0.4).astype(np.float32), qt)
+        assert np.float32(f.vec_dot(4096, w, q)).view(np.uint32) == np.float32(ref.vec_dot(qt, 4096, w, q)).view(np.uint32)
+    assert not lvk.QuantizeFns(6).valid          # GGML_TYPE_F32: no codec entry
