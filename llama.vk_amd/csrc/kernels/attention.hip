@@ -10,6 +10,12 @@
 //   then the merged heads are quantized to the Wo weight format here, so the
 //   Wo matvec reads 20 B/block instead of 128 B of f32.
 //
+// With the f32 KV cache (f16_kv = false, llama.cpp:1614) the same kernel runs F32 = true:
+// KQ = mul_mat(K_view f32, Q f32) and KQV = mul_mat(V_view f32, P f32) are
+// ggml_compute_forward_mul_mat_f32 (ggml.c:6134-6297), i.e. ggml_vec_dot_f32
+// (ggml.c:1713-1748): the same 4 x 8 accumulators and reduce, no f16 rounding of Q or P,
+// leftovers summed in float.
+//
 // ggml_vec_dot_f16 structure reproduced: element i of a 32-wide step feeds
 // accumulator (r, l) = (i/8, i%8) of 4 AVX registers x 8 lanes via fmaf; the
 // reduce is (s0+s1)+(s2+s3) per lane l, then t_l = S[l]+S[l+4] (l<4), then
@@ -88,7 +94,31 @@ __global__ void k_exp_check(const uint16_t * __restrict__ tab, int * __restrict_
 //   phase 4  quantize the HD/2 outputs (HD/64 weight blocks) for Wo
 // grid (H, N, 2), 256 threads.
 // ---------------------------------------------------------------------------
-template <int HD, int QT>
+// 8 elements of a step from one 16-byte (f16) or two 16-byte (f32) loads
+template <bool F32> struct Vec8 { uint4 w[F32 ? 2 : 1]; };
+template <bool F32>
+__device__ __forceinline__ Vec8<F32> ld8(const uint16_t * base, size_t elem) {
+    Vec8<F32> v;
+    if constexpr (F32) {
+        const uint4 * p = (const uint4 *) ((const float *) base + elem);
+        v.w[0] = p[0]; v.w[1] = p[1];
+    } else {
+        v.w[0] = *(const uint4 *) (base + elem);
+    }
+    return v;
+}
+template <bool F32>
+__device__ __forceinline__ void unpack8(const Vec8<F32> & v, float f[8]) {
+    if constexpr (F32) {
+        const uint32_t w[8] = {v.w[0].x, v.w[0].y, v.w[0].z, v.w[0].w, v.w[1].x, v.w[1].y, v.w[1].z, v.w[1].w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] = __uint_as_float(w[k]);
+    } else {
+        unpack8h(v.w[0], f);
+    }
+}
+
+template <int HD, int QT, bool F32>
 __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16, const uint16_t * __restrict__ kc,
                                               const uint16_t * __restrict__ vc, const uint16_t * __restrict__ exp_tab,
                                               ActQ out, const StepParams * sp, int E, int n_ctx, float scale,
@@ -111,39 +141,44 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
     // 64 positions, a lane quad per position) and of V (16 steps of 32
     // positions for this thread's output dim).  Nothing here depends on the
     // softmax, so one memory round trip covers the whole kernel at n_kv <= 512.
-    constexpr int KP = 8, VS = 16, PB = KP * 64;
-    uint4 qv[NSTEP];
-    {
-        const uint4 * qp = (const uint4 *) (q16 + (size_t) t * E + h * HD) + r;
+    constexpr int KP = F32 ? 4 : 8, VS = F32 ? 8 : 16, PB = KP * 64;
+    constexpr int VSB = F32 ? 8192 : 4096;            // LDS bytes per V step of 64 dims x 32 positions
+    Vec8<F32> qv[NSTEP];
 #pragma unroll
-        for (int st = 0; st < NSTEP; ++st) qv[st] = qp[st * 4];
-    }
+    for (int st = 0; st < NSTEP; ++st) qv[st] = ld8<F32>(q16, (size_t) t * E + h * HD + st * 32 + r * 8);
     const int npos = min(n_kv, lim + 1);     // masked positions get -inf without a dot
-    uint4 kv[KP][NSTEP];
+    Vec8<F32> kv[KP][NSTEP];
     auto load_k = [&](int pb) {
 #pragma unroll
         for (int ps = 0; ps < KP; ++ps) {
             if (pb + ps * 64 < npos) {          // wave-uniform: no duplicate requests past n_kv
                 const int pp = min(pb + ps * 64 + (tid >> 2), npos - 1);
-                const uint4 * kp = (const uint4 *) (kc + (size_t) pp * E + h * HD) + r;
 #pragma unroll
-                for (int st = 0; st < NSTEP; ++st) kv[ps][st] = kp[st * 4];
+                for (int st = 0; st < NSTEP; ++st) kv[ps][st] = ld8<F32>(kc, (size_t) pp * E + h * HD + st * 32 + r * 8);
             }
         }
     };
     const int d = half * (HD / 2) + (tid >> 2);
-    const uint16_t * vrow = vc + (size_t) (h * HD + d) * n_ctx;
+    const size_t vrow = (size_t) (h * HD + d) * n_ctx;   // element offset of this thread's V row
     const int np = n_kv & ~31;
     const int nvs = (n_kv + 31) / 32;                  // V steps including a partial one
-    // V steps 0..VS-1 go to LDS by DMA: step s of the workgroup's 64 dims is
-    // 4 KiB at vlds + s*4096, thread tid's 16 bytes at + tid*16
+    // V steps 0..VS-1 go to LDS by DMA: step s of the workgroup's 64 dims is VSB bytes at
+    // vlds + s*VSB, thread tid's first 16 bytes at + tid*16 (f32: the second at + 4096 + tid*16)
     uint8_t * vlds = smem + (size_t) n_ctx * 6 + 64;
     LVK_AT(0);
     load_k(0);
     {
         uint8_t * vl = vlds + (tid & ~63) * 16;       // wave-uniform base
         const int nd = min(nvs, VS);
-        for (int st = 0; st < nd; ++st) dma16(vrow + (size_t) st * 32 + r * 8, vl + st * 4096);
+        for (int st = 0; st < nd; ++st) {
+            if constexpr (F32) {
+                const float * vf = (const float *) vc + vrow + (size_t) st * 32 + r * 8;
+                dma16(vf, vl + st * VSB);
+                dma16(vf + 4, vl + st * VSB + 4096);
+            } else {
+                dma16(vc + vrow + (size_t) st * 32 + r * 8, vl + st * VSB);
+            }
+        }
     }
     LVK_AT(1);
 
@@ -157,8 +192,8 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
 #pragma unroll
                 for (int st = 0; st < NSTEP; ++st) {
                     float kf[8], qf[8];
-                    unpack8h(kv[ps][st], kf);
-                    unpack8h(qv[st], qf);
+                    unpack8<F32>(kv[ps][st], kf);
+                    unpack8<F32>(qv[st], qf);
 #pragma unroll
                     for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(kf[l], qf[l], s[l]);
                 }
@@ -200,9 +235,13 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
     sum = (redd[0] + redd[1]) + (redd[2] + redd[3]);
     const float scl = (float) (1.0 / sum);
     const int n_pad = (n_kv + 31) & ~31;
-    for (int p = tid; p < n_pad; p += 256) p16[p] = p < n_kv ? f32_to_f16(sc[p] * scl) : (uint16_t) 0;
+    if constexpr (F32) {
+        for (int p = tid; p < n_pad; p += 256) sc[p] = p < n_kv ? sc[p] * scl : 0.0f;   // P stays f32
+    } else {
+        for (int p = tid; p < n_pad; p += 256) p16[p] = p < n_kv ? f32_to_f16(sc[p] * scl) : (uint16_t) 0;
+    }
     __syncthreads();
-    if (p16_out && half == 0)
+    if (!F32 && p16_out && half == 0)
         for (int p = tid; p < n_kv; p += 256) p16_out[((size_t) t * gridDim.x + h) * n_ctx + p] = p16[p];
 
     LVK_AT(3);
@@ -210,30 +249,49 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t * __restrict__ q16,
     __syncthreads();     // vmcnt(0) + barrier: every wave's V DMA has landed
     const int nsteps = min(np, lim + 1 + 31) / 32;     // steps holding at least one unmasked position
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    auto pv_step = [&](const uint4 v4, int st) {
+    auto pv_step = [&](const Vec8<F32> & v8, int st) {
         float vf[8], pf[8];
-        unpack8h(v4, vf);
-        unpack8h(*((const uint4 *) (p16 + st * 32) + r), pf);
+        unpack8<F32>(v8, vf);
+        if constexpr (F32) {
+#pragma unroll
+            for (int l = 0; l < 8; ++l) pf[l] = sc[st * 32 + r * 8 + l];
+        } else {
+            unpack8h(*((const uint4 *) (p16 + st * 32) + r), pf);
+        }
 #pragma unroll
         for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(vf[l], pf[l], s[l]);
     };
     const int nl = min(nsteps, VS);
-    for (int st = 0; st < nl; ++st) pv_step(*((const uint4 *) (vlds + (size_t) st * 4096) + tid), st);
-    for (int st = VS; st < nsteps; ++st) pv_step(*((const uint4 *) (vrow + (size_t) st * 32) + r), st);
+    for (int st = 0; st < nl; ++st) {
+        Vec8<F32> v8;
+        v8.w[0] = *((const uint4 *) (vlds + (size_t) st * VSB) + tid);
+        if constexpr (F32) v8.w[1] = *((const uint4 *) (vlds + (size_t) st * VSB + 4096) + tid);
+        pv_step(v8, st);
+    }
+    for (int st = VS; st < nsteps; ++st) pv_step(ld8<F32>(vc, vrow + (size_t) st * 32 + r * 8), st);
     const float res = quad_f16dot_reduce(s);
     float o = res;
-    if (np < n_kv && np <= lim) {
+    if (F32 && np < n_kv && np <= lim) {
+        // leftovers in float, in position order (ggml.c:1736-1739: sumf += x[i]*y[i])
+        if (r == 0) {
+            const int ne = min(n_kv, lim + 1);
+            const float * vrf = (const float *) vc + vrow;
+            float sumf = res;
+            for (int i = np; i < ne; ++i) { const float pr = vrf[i] * sc[i]; sumf = sumf + pr; }
+            o = sumf;
+        }
+    } else if (!F32 && np < n_kv && np <= lim) {
         // leftovers in double, in position order (ggml.c:1806-1808), from registers
         const int ts = np / 32;
         uint4 vt[4], pt[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             pt[k] = *((const uint4 *) (p16 + np) + k);
-            if (ts < VS) vt[k] = *((const uint4 *) (vlds + (size_t) ts * 4096) + (tid & ~3) + k);
+            if (ts < VS) vt[k] = *((const uint4 *) (vlds + (size_t) ts * VSB) + (tid & ~3) + k);
         }
         if (ts >= VS)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) vt[k] = *((const uint4 *) (vrow + np) + k);
+            for (int k = 0; k < 4; ++k) vt[k] = *((const uint4 *) (vc + vrow + np) + k);
         if (r == 0) {
             const int nt_ = min(n_kv, lim + 1) - np;
             double sumf = (double) res;
@@ -313,17 +371,21 @@ hipError_t exp_check(const uint16_t * exp_tab, int * bad_d, hipStream_t s) {
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s) {
     const int hd = A.n_embd / A.n_head;
     if (hd != 128 || A.n_ctx % 32 || A.n_ctx < 128) return hipErrorInvalidValue;
+    if (A.kv32 && A.p16_out) return hipErrorInvalidValue;
     if (A.out_qtype != Q4_0 && A.out_qtype != Q4_1) return hipErrorNotSupported;
     const float scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
     dim3 grid(A.n_head, A.n_tokens, 2);
     // scores, P16, reductions, then V steps 0..15 by DMA (4 KiB each)
     const size_t lds = (size_t) A.n_ctx * 6 + 64 + 16 * 4096;
-    if (A.out_qtype == Q4_1)
-        LVK_LAUNCH((k_attn<128, Q4_1>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,
-                   A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out, A.exp_computed);
-    else
-        LVK_LAUNCH((k_attn<128, Q4_0>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,
-                   A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out, A.exp_computed);
+#define LVK_ATTN_GO(QT_, F32_)                                                                                  \
+    LVK_LAUNCH((k_attn<128, QT_, F32_>), grid, dim3(256), lds, s, A.q16, A.kc, A.vc, A.exp_tab, A.out, A.sp,  \
+               A.n_embd, A.n_ctx, scale, A.scores, A.out_f32, A.p16_out, A.exp_computed)
+    if (A.out_qtype == Q4_1) {
+        if (A.kv32) LVK_ATTN_GO(Q4_1, true); else LVK_ATTN_GO(Q4_1, false);
+    } else {
+        if (A.kv32) LVK_ATTN_GO(Q4_0, true); else LVK_ATTN_GO(Q4_0, false);
+    }
+#undef LVK_ATTN_GO
     return hipGetLastError();
 }
 

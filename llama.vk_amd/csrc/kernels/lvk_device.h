@@ -27,6 +27,14 @@ __device__ __forceinline__ float f16_to_f32(uint16_t h) {
     return (float) __builtin_bit_cast(_Float16, h);   // exact
 }
 
+// KV-cache / query element store: f16 (the reference's f32 -> f16 cpy, RNE) or, with the
+// f32 KV cache (llama_context_params.f16_kv = false, llama.cpp:1614), the f32 value itself;
+// `base` then addresses floats (the buffer is sized for 4-byte elements)
+__device__ __forceinline__ void kv_store(uint16_t * base, size_t i, float v, int f32) {
+    if (f32) ((float *) base)[i] = v;
+    else base[i] = f32_to_f16(v);
+}
+
 // table_exp_f16[h] (ggml.c:2915-2927: fp16(expf(fp16->f32(h))), built with the
 // host's glibc) for the arguments softmax produces (h <= 0, not NaN).
 // mode 0 reads the uploaded table; mode 1 computes exp in double, mode 2 with

@@ -104,6 +104,7 @@ struct MvLaunch {
     uint16_t * vc = nullptr;         // layer V cache [E][n_ctx]
     RopeTable rope{};
     int n_embd = 0, head_dim = 0, n_ctx = 0;
+    int kv32 = 0;                    // f32 KV cache and f32 queries (f16_kv = false)
     // EPI_SWIGLU
     const uint16_t * silu_tab = nullptr;   // 64Ki fp16 table
     ActQ out_q;                            // quantized u = silu(w1 x) * (w3 x)
@@ -143,6 +144,7 @@ struct AttnLaunch {
     uint16_t * p16_out = nullptr; // optional (debug): f16 probabilities [N][H][n_ctx]
     int exp_computed = 0;     // exp mode (lvk_device.h exp_f16): 0 table, 1 double, 2 f32 -- nonzero only after exp_check
     unsigned * err = nullptr; // host-mapped error word (DevError); kernels that spin report a timeout here
+    int kv32 = 0;             // f32 K, V and queries (f16_kv = false): launch_attention only
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
 // prompt batches (N > 1, Q4_0 output): scores+softmax per (head, 32 tokens) then
@@ -198,7 +200,7 @@ hipError_t launch_act_f16(const float * x, const float * g, int N, int K, void *
 hipError_t launch_actq_to_f16(const ActQ & q, int N, int K, void * xm, float * da, hipStream_t s);
 // RoPE + KV append of stored Q|K|V rows qkv [N][3E]
 hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 * rope, const StepParams * sp,
-                          int n_ctx, uint16_t * q16, uint16_t * kc, uint16_t * vc, hipStream_t s);
+                          int n_ctx, uint16_t * q16, uint16_t * kc, uint16_t * vc, hipStream_t s, int kv32 = 0);
 
 // operator-level helpers used by the C ABI tests
 hipError_t launch_quantize_act(const float * x, int N, int K, int qtype, ActQ out, hipStream_t s);

@@ -52,6 +52,7 @@ struct CuParams {
     uint16_t * vc;
     const float2 * rope;
     int n_embd, head_dim, n_ctx;
+    int kv32;                   // f32 KV cache and queries (f16_kv = false)
     const uint16_t * silu_tab;
 };
 
@@ -375,10 +376,10 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
                     float out;
                     if ((i0 & 1) == 0) { const float a = res * cs.x, b = other * cs.y; out = a - b; }
                     else               { const float a = other * cs.y, b = res * cs.x; out = a + b; }
-                    if (which == 0) P.q16[e] = f32_to_f16(out);
-                    else            P.kc[(size_t) pos * E + e] = f32_to_f16(out);
+                    if (which == 0) kv_store(P.q16, e, out, P.kv32);
+                    else            kv_store(P.kc, (size_t) pos * E + e, out, P.kv32);
                 } else {
-                    P.vc[(size_t) e * P.n_ctx + pos] = f32_to_f16(res);
+                    kv_store(P.vc, (size_t) e * P.n_ctx + pos, res, P.kv32);
                 }
             }
         } else if constexpr (EPI == EPI_SWIGLU_F32) {
@@ -458,7 +459,7 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
     P.y = L.y ? L.y + (size_t) L.out_tok0 * L.w.M : nullptr;
     P.u = L.u;
     P.q16 = L.q16; P.kc = L.kc; P.vc = L.vc; P.rope = L.rope.cs;
-    P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx;
+    P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx; P.kv32 = L.kv32;
     P.silu_tab = L.silu_tab;
     const int K = L.w.K;
 #ifdef LVK_PROBE_SWEEP   // dev probe builds only: LVK_CFG selects a launch shape

@@ -50,6 +50,7 @@ struct Params {
     uint16_t * vc;
     const float2 * rope;
     int n_embd, head_dim, n_ctx;
+    int kv32;                   // f32 KV cache and queries (f16_kv = false)
     const uint16_t * silu_tab;
     ActQ out_q;
 };
@@ -367,10 +368,10 @@ __global__ __launch_bounds__(NT) void k_matvec_q40(Params P) {
                     float out;
                     if ((i0 & 1) == 0) { const float a = res[tt] * cs.x, b = other * cs.y; out = a - b; }
                     else               { const float a = other * cs.y, b = res[tt] * cs.x; out = a + b; }
-                    if (which == 0) P.q16[(size_t) (t0 + tt) * E + e] = f32_to_f16(out);
-                    else            P.kc[(size_t) pos * E + e] = f32_to_f16(out);
+                    if (which == 0) kv_store(P.q16, (size_t) (t0 + tt) * E + e, out, P.kv32);
+                    else            kv_store(P.kc, (size_t) pos * E + e, out, P.kv32);
                 } else {
-                    P.vc[(size_t) e * P.n_ctx + pos] = f32_to_f16(res[tt]);
+                    kv_store(P.vc, (size_t) e * P.n_ctx + pos, res[tt], P.kv32);
                 }
             }
         }
@@ -438,7 +439,7 @@ hipError_t launch_matvec(const MvLaunch & L, int pro, int epi, hipStream_t s) {
     P.x = L.x; P.g = L.g; P.xq = L.xq; P.sp = L.sp;
     P.n_tokens = L.n_tokens; P.tok0 = L.tok0; P.out_tok0 = L.out_tok0;
     P.y = L.y; P.q16 = L.q16; P.kc = L.kc; P.vc = L.vc; P.rope = L.rope.cs;
-    P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx;
+    P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx; P.kv32 = L.kv32;
     P.silu_tab = L.silu_tab; P.out_q = L.out_q;
     const int ng = L.w.M / 8;
     const int N = L.n_tokens;

@@ -436,7 +436,7 @@ __global__ void k_actq_to_f16(ActQ q, int N, int K, uint2 * __restrict__ xm, flo
 // stored Q|K|V rows [N][3E] -> q16 [N][E], K cache [pos][E], V cache [E][pos]
 __global__ void k_rope_kv(const float * __restrict__ qkv, int N, int E, int hd, const float2 * __restrict__ rope,
                           const StepParams * __restrict__ sp, int n_ctx, uint16_t * __restrict__ q16,
-                          uint16_t * __restrict__ kc, uint16_t * __restrict__ vc) {
+                          uint16_t * __restrict__ kc, uint16_t * __restrict__ vc, int kv32) {
     const int t = blockIdx.y;
     const int e2 = blockIdx.x * blockDim.x + threadIdx.x;     // pair index over Q|K (E/2 each) then V
     const int pos = sp->n_past + t;
@@ -452,16 +452,16 @@ __global__ void k_rope_kv(const float * __restrict__ qkv, int N, int E, int hd, 
         const float a1 = x0 * cs.y, b1 = x1 * cs.x;
         const float o1 = a1 + b1;
         if (which == 0) {
-            q16[(size_t) t * E + e] = f32_to_f16(o0);
-            q16[(size_t) t * E + e + 1] = f32_to_f16(o1);
+            kv_store(q16, (size_t) t * E + e, o0, kv32);
+            kv_store(q16, (size_t) t * E + e + 1, o1, kv32);
         } else {
-            kc[(size_t) pos * E + e] = f32_to_f16(o0);
-            kc[(size_t) pos * E + e + 1] = f32_to_f16(o1);
+            kv_store(kc, (size_t) pos * E + e, o0, kv32);
+            kv_store(kc, (size_t) pos * E + e + 1, o1, kv32);
         }
     } else if (e2 < E + E / 2) {
         const int e = 2 * (e2 - E);
-        vc[(size_t) e * n_ctx + pos] = f32_to_f16(row[2 * E + e]);
-        vc[(size_t) (e + 1) * n_ctx + pos] = f32_to_f16(row[2 * E + e + 1]);
+        kv_store(vc, (size_t) e * n_ctx + pos, row[2 * E + e], kv32);
+        kv_store(vc, (size_t) (e + 1) * n_ctx + pos, row[2 * E + e + 1], kv32);
     }
 }
 
@@ -505,9 +505,10 @@ hipError_t launch_actq_to_f16(const ActQ & q, int N, int K, void * xm, float * d
 }
 
 hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 * rope, const StepParams * sp,
-                          int n_ctx, uint16_t * q16, uint16_t * kc, uint16_t * vc, hipStream_t s) {
+                          int n_ctx, uint16_t * q16, uint16_t * kc, uint16_t * vc, hipStream_t s, int kv32) {
     const int pairs = E + E / 2;
-    LVK_LAUNCH(k_rope_kv, dim3((pairs + 255) / 256, N), dim3(256), 0, s, qkv, N, E, hd, rope, sp, n_ctx, q16, kc, vc);
+    LVK_LAUNCH(k_rope_kv, dim3((pairs + 255) / 256, N), dim3(256), 0, s, qkv, N, E, hd, rope, sp, n_ctx, q16, kc, vc,
+               kv32);
     return hipGetLastError();
 }
 

@@ -219,8 +219,6 @@ struct StageProgress {
 // load layers [layer_begin, layer_end) of the file into c on the current HIP device
 static void load_stage(lvk::Context & c, const char * path_model, const llama_context_params & params, int layer_begin,
                        int layer_end, void (*progress)(float, void *), void * progress_ud) {
-    if (!params.f16_kv && !params.vocab_only)
-        fprintf(stderr, "llama.vk_amd: f32 KV cache not implemented on the GPU path; using f16 KV\n");
     hipStream_t ls = nullptr;
     if (!params.vocab_only) LVK_HIP(hipStreamCreateWithFlags(&ls, hipStreamNonBlocking));
     struct StreamFree { hipStream_t s; ~StreamFree() { if (s) (void) hipStreamDestroy(s); } } ls_guard{ls};

@@ -77,19 +77,26 @@ Context::~Context() {
 }
 
 void Context::init(const llama_context_params & p) {
-    n_ctx = p.n_ctx;
+    // the caller's window (llama.h accepts any positive n_ctx); buffers and kernels use it
+    // rounded up to the 32-position attention tile, at least 128 (positions past the
+    // caller's window are never written or read)
+    if (p.n_ctx <= 0) throw Error("llama.vk_amd: n_ctx must be positive");
+    n_ctx_user = p.n_ctx;
+    n_ctx = std::max(128, (p.n_ctx + 31) / 32 * 32);
     logits_all = p.logits_all;
     want_embedding = p.embedding;
     const HParams & hp = model.hp;
     const size_t E = hp.n_embd, L = model.layers.size(), V = hp.n_vocab, H = hp.n_head, F = hp.n_ff();
     const size_t hd = E / H, C = (size_t) n_ctx;
-    if (n_ctx < 64 || n_ctx % 32) throw Error("llama.vk_amd: n_ctx must be a multiple of 32 and >= 64");
-    kc = (uint16_t *) model.alloc(L * C * E * 2);
-    vc = (uint16_t *) model.alloc(L * C * E * 2);
-    LVK_HIP(hipMemset(kc, 0, L * C * E * 2));
-    LVK_HIP(hipMemset(vc, 0, L * C * E * 2));
+    // KV cache element type (llama.cpp:1614): f16, or f32 when the caller asks for it
+    kv32 = !p.f16_kv;
+    const size_t es = kv_elem_bytes();
+    kc = (uint16_t *) model.alloc(L * C * E * es);
+    vc = (uint16_t *) model.alloc(L * C * E * es);
+    LVK_HIP(hipMemset(kc, 0, L * C * E * es));
+    LVK_HIP(hipMemset(vc, 0, L * C * E * es));
     x = (float *) model.alloc(C * E * 4);
-    q16 = (uint16_t *) model.alloc(C * E * 2);
+    q16 = (uint16_t *) model.alloc(C * E * es);      // queries in the KV element type
     scores = (float *) model.alloc(C * H * C * 4);
     aq_attn.nb = (int) (E / 32);
     aq_attn.d = (float *) model.alloc(C * (E / 32) * 4);
@@ -126,8 +133,8 @@ void Context::init(const llama_context_params & p) {
             for (int k = 0; k < 4; ++k) { tl[il].nib[k] = m4[k]->nib; tl[il].scl[k] = (const float4 *) m4[k]->scl; }
             tl[il].attn_norm = ly.attn_norm;
             tl[il].ffn_norm = ly.ffn_norm;
-            tl[il].kc = kc + il * C * E;
-            tl[il].vc = vc + il * C * E;
+            tl[il].kc = kc_layer(il);
+            tl[il].vc = vc_layer(il);
         }
         dlayers = (DecodeLayer *) model.alloc(std::max<size_t>(1, L) * sizeof(DecodeLayer));
         if (L) LVK_HIP(hipMemcpy(dlayers, tl.data(), L * sizeof(DecodeLayer), hipMemcpyHostToDevice));
@@ -233,7 +240,7 @@ bool Context::persistent_ok() const { return decode_persistent && dargs_d != nul
 // the persistent kernel's arguments never change for a context: built and uploaded once
 void Context::prepare_persistent() {
     const HParams & hp = model.hp;
-    if (model.layers.empty() || model.qtype != Q4_0) return;
+    if (model.layers.empty() || model.qtype != Q4_0 || kv32) return;
     DecodeArgs A{};
     A.layers = dlayers;
     A.n_layer = (int) model.layers.size();
@@ -295,7 +302,6 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
     if (!tok_src) tok_src = tok_d;
     float * const logits_out = logits_d + (size_t) logit_row * hp.n_vocab;
     const int E = (int) hp.n_embd, H = (int) hp.n_head, hd = E / H, F = (int) hp.n_ff();
-    const size_t CE = (size_t) n_ctx * E;
     if (use_mfma(n)) {
         // prompt batch on the matrix cores: per layer
         //   act(norm) -> QKV (store) -> RoPE + KV append -> attention -> act -> Wo (+x)
@@ -304,19 +310,20 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
             timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_src, n, x, stream); });
         for (size_t il = 0; il < model.layers.size(); ++il) {
             const Layer & ly = model.layers[il];
-            uint16_t * kcl = kc + il * CE;
-            uint16_t * vcl = vc + il * CE;
+            uint16_t * kcl = kc_layer(il);
+            uint16_t * vcl = vc_layer(il);
             timed_launch(K_QKV, 0, [&] { return launch_act_f16(x, ly.attn_norm, n, E, xh, xda, stream); });
             timed_launch(K_QKV, qbytes(ly.wqkv), [&] {
                 return launch_mm_mfma(ly.wqkv, xh, xda, n, qkv32, 3 * E, 0, EPI_STORE, nullptr, stream);
             });
             timed_launch(K_QKV, 0, [&] {
-                return launch_rope_kv(qkv32, n, E, hd, rope, sp_d, n_ctx, q16, kcl, vcl, stream);
+                return launch_rope_kv(qkv32, n, E, hd, rope, sp_d, n_ctx, q16, kcl, vcl, stream, kv32);
             });
             AttnLaunch at{q16, kcl, vcl, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
             at.exp_computed = exp_computed;
             at.err = err_d;
-            if (attention_prompt_supported(E, H, n_ctx)) {
+            at.kv32 = kv32;
+            if (!kv32 && attention_prompt_supported(E, H, n_ctx)) {
                 // writes the Wo input in both forms (ActQ and the MFMA fragment image)
                 timed_launch(K_ATTN, 0, [&] {
                     return launch_attention_prompt(at, (uint16_t *) scores, xh, xda, stream);
@@ -367,7 +374,7 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
     // single-token FFN: W1|W3 hands silu(w1 x)*(w3 x) to W2 in f32, W2 quantizes it
     const bool ffn_f32 = n == 1 && matvec_cu_supported(E, model.qtype) && matvec_cu_supported(F, model.qtype);
     // attention, Wo and the residual add in one launch (attention_decode.hip, k_attn_wo)
-    const bool attn_wo = n == 1 && !old_attention && fuse_attn_wo && model.qtype == Q4_0 && !model.layers.empty() &&
+    const bool attn_wo = n == 1 && !old_attention && !kv32 && fuse_attn_wo && model.qtype == Q4_0 && !model.layers.empty() &&
                          attention_wo_supported(E, H, n_ctx, model.layers[0].wo);
     if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx))
         // the decode attention's score granules carry epoch = layer + 1: zero them once per token
@@ -381,22 +388,23 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
         const Layer & ly = model.layers[il];
         MvLaunch a;
         a.w = ly.wqkv; a.x = x; a.g = ly.attn_norm; a.sp = sp_d; a.n_tokens = n;
-        a.q16 = q16; a.kc = kc + il * CE; a.vc = vc + il * CE; a.rope.cs = rope;
-        a.n_embd = E; a.head_dim = hd; a.n_ctx = n_ctx;
+        a.q16 = q16; a.kc = kc_layer(il); a.vc = vc_layer(il); a.rope.cs = rope;
+        a.n_embd = E; a.head_dim = hd; a.n_ctx = n_ctx; a.kv32 = kv32;
         timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
-        AttnLaunch at{q16, kc + il * CE, vc + il * CE, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
+        AttnLaunch at{q16, kc_layer(il), vc_layer(il), scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
         at.exp_computed = exp_computed;
         at.err = err_d;
+        at.kv32 = kv32;
         if (attn_wo) {
             timed_launch(K_ATTN_WO, qbytes(ly.wo), [&] {
                 return launch_attention_wo(at, ly.wo, x, attn_gran, (unsigned) il + 1, stream);
             });
         } else {
-            if (n > 1 && model.qtype == Q4_0 && attention_prompt_supported(E, H, n_ctx))
+            if (n > 1 && !kv32 && model.qtype == Q4_0 && attention_prompt_supported(E, H, n_ctx))
                 timed_launch(K_ATTN, 0, [&] {
                     return launch_attention_prompt(at, (uint16_t *) scores, nullptr, nullptr, stream);
                 });
-            else if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx))
+            else if (n == 1 && !old_attention && !kv32 && attention_decode_supported(E, H, n_ctx))
                 timed_launch(K_ATTN, 0, [&] { return launch_attention_decode(at, attn_gran, (unsigned) il + 1, stream); });
             else
                 timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
@@ -504,7 +512,7 @@ void Context::begin_eval(const int * tokens, int n, int n_past, const EvalPart &
     const HParams & hp = model.hp;
     const int V = (int) hp.n_vocab;
     const int n_total = part.n_total < 0 ? n : part.n_total;
-    if (n <= 0 || n_past < 0 || n_past + n > n_ctx || part.tok_off < 0 || part.tok_off + n > n_total)
+    if (n <= 0 || n_past < 0 || n_past + n > n_ctx_user || part.tok_off < 0 || part.tok_off + n > n_total)
         throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
     if ((part.greedy || part.sample) && (!model.has_head || n != 1 || logits_all))
         throw Error("llama.vk_amd: greedy / sampling eval needs the lm_head stage, one token and last-token logits");
@@ -563,7 +571,7 @@ void Context::end_eval(bool no_host_logits) {
 }
 
 size_t Context::kv_bytes() const {
-    return 2u * (size_t) model.layers.size() * n_ctx * model.hp.n_embd * 2u;
+    return 2u * (size_t) model.layers.size() * n_ctx * model.hp.n_embd * kv_elem_bytes();
 }
 
 void Context::kv_get() {
@@ -586,7 +594,7 @@ void Context::kv_set(const uint8_t * src, size_t n) {
 // (layer, dim).  Only the n_tokens positions move, not the whole cache.
 void Context::kv_copy_from(const Context & src, int n_tokens) {
     const size_t E = model.hp.n_embd, L = model.layers.size(), C = (size_t) n_ctx;
-    if (src.model.hp.n_embd != model.hp.n_embd || src.model.layers.size() != L || src.n_ctx != n_ctx ||
+    if (src.model.hp.n_embd != model.hp.n_embd || src.model.layers.size() != L || src.n_ctx != n_ctx || src.n_ctx_user != n_ctx_user ||
         src.model.hp.n_head != model.hp.n_head || src.model.layer_begin != model.layer_begin)
         throw Error("lvk_kv_copy: contexts differ in n_embd, n_head, n_layer, layer range or n_ctx");
     if (src.device != device) throw Error("lvk_kv_copy: contexts live on different HIP devices");
@@ -594,12 +602,14 @@ void Context::kv_copy_from(const Context & src, int n_tokens) {
     // file contents (size and quantization type are checked; the caller owns identity)
     if (src.model.qtype != model.qtype || src.model.file_bytes != model.file_bytes)
         throw Error("lvk_kv_copy: contexts hold different models");
-    if (n_tokens < 0 || n_tokens > n_ctx) throw Error("lvk_kv_copy: n_tokens out of range");
+    if (src.kv32 != kv32) throw Error("lvk_kv_copy: contexts differ in the KV cache type (f16_kv)");
+    if (n_tokens < 0 || n_tokens > n_ctx_user) throw Error("lvk_kv_copy: n_tokens out of range");
     if (n_tokens > 0) {
         const size_t n = (size_t) n_tokens;
         LVK_HIP(hipStreamSynchronize(src.stream));
-        LVK_HIP(hipMemcpy2DAsync(kc, C * E * 2, src.kc, C * E * 2, n * E * 2, L, hipMemcpyDeviceToDevice, stream));
-        LVK_HIP(hipMemcpy2DAsync(vc, C * 2, src.vc, C * 2, n * 2, L * E, hipMemcpyDeviceToDevice, stream));
+        const size_t es = kv_elem_bytes();
+        LVK_HIP(hipMemcpy2DAsync(kc, C * E * es, src.kc, C * E * es, n * E * es, L, hipMemcpyDeviceToDevice, stream));
+        LVK_HIP(hipMemcpy2DAsync(vc, C * es, src.vc, C * es, n * es, L * E, hipMemcpyDeviceToDevice, stream));
         LVK_HIP(hipStreamSynchronize(stream));
     }
     kv_n = n_tokens;

@@ -60,14 +60,19 @@ struct EvalPart {
 
 struct Context {
     Model model;
-    int n_ctx = 512;
+    int n_ctx = 512;             // allocated positions (the caller's n_ctx rounded up to 32, >= 128)
+    int n_ctx_user = 512;        // llama_context_params.n_ctx: the positions an eval may use
     bool logits_all = false;
     bool want_embedding = false;
     hipStream_t stream = nullptr;
 
     // device state
-    uint16_t * kc = nullptr;     // [L][n_ctx][E]
-    uint16_t * vc = nullptr;     // [L][E][n_ctx]
+    uint16_t * kc = nullptr;     // [L][n_ctx][E] f16, or f32 when kv32
+    uint16_t * vc = nullptr;     // [L][E][n_ctx] f16, or f32 when kv32
+    bool kv32 = false;           // f32 KV cache and queries (llama_context_params.f16_kv = false)
+    size_t kv_elem_bytes() const { return kv32 ? 4 : 2; }
+    uint16_t * kc_layer(size_t il) const { return kc + il * (size_t) n_ctx * model.hp.n_embd * (kv_elem_bytes() / 2); }
+    uint16_t * vc_layer(size_t il) const { return vc + il * (size_t) n_ctx * model.hp.n_embd * (kv_elem_bytes() / 2); }
     float * x = nullptr;         // residual stream [n_ctx][E]
     uint16_t * q16 = nullptr;    // [n_ctx][E]
     float * scores = nullptr;    // [n_ctx][H][n_ctx]

@@ -119,7 +119,7 @@ void Split::hop(int s, int n) {
 void Split::eval(const int * tokens, int n, int n_past, bool greedy) {
     const int S = (int) st.size();
     Context & last = *st.back();
-    if (n <= 0 || n_past < 0 || n_past + n > last.n_ctx) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
+    if (n <= 0 || n_past < 0 || n_past + n > last.n_ctx_user) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
     const int m = (micro > 0 && n > micro) ? micro : n;
     std::string err;
     try {
@@ -203,7 +203,7 @@ int stage_step(Context & c, const int * tokens, int n, int n_past, bool greedy, 
     StageLink & L = *c.link;
     const int s = L.stage, S = L.n_stages;
     if (greedy && n != 1) throw Error("llama.vk_amd: a greedy stage step takes one token");
-    if (n <= 0 || n_past < 0 || n_past + n > c.n_ctx) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
+    if (n <= 0 || n_past < 0 || n_past + n > c.n_ctx_user) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
     const int m = (micro > 0 && n > micro) ? micro : n;
     const size_t E = c.model.hp.n_embd;
     DeviceGuard g(c.device);

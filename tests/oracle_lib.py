@@ -151,15 +151,15 @@ class Ref:
     def vec_dot(self, qtype, k, x, y):
         return self.lib.ref_vec_dot(qtype, k, x, y)
 
-    def model(self, path, n_ctx=512, logits_all=False):
-        return RefModel(self, path, n_ctx, logits_all)
+    def model(self, path, n_ctx=512, logits_all=False, f16_kv=True):
+        return RefModel(self, path, n_ctx, logits_all, f16_kv)
 
 
 class RefModel:
-    def __init__(self, ref, path, n_ctx, logits_all):
+    def __init__(self, ref, path, n_ctx, logits_all, f16_kv=True):
         self.ref = ref
         self.logits_all = logits_all
-        self.h = ref.lib.ref_open(path.encode(), n_ctx, 1, int(logits_all), 1)
+        self.h = ref.lib.ref_open(path.encode(), n_ctx, int(f16_kv), int(logits_all), 1)
         if not self.h:
             raise RuntimeError("reference failed to load %s" % path)
         self.n_vocab = ref.lib.ref_n_vocab(self.h)
