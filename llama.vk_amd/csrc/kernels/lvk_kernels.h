@@ -180,8 +180,16 @@ hipError_t launch_repack(const void * src_rows, int qtype, int M, int K, uint4 *
                          hipStream_t s, int interleave4 = 0);
 // bytes of the two image arrays for an M x K matrix
 inline size_t qimage_nib_bytes(int M, int K) { return (size_t) M * ((K / 32 + 31) / 32) * 512; }
+// Q4_1: d and m images, then the even-chain weight-sum image (q41_wsum)
 inline size_t qimage_scl_bytes(int M, int K, int qtype = Q4_0) {
-    return (size_t) M * ((K / 32 + 31) / 32) * 128 * (qtype == Q4_1 ? 2 : 1);
+    return (size_t) M * ((K / 32 + 31) / 32) * 128 * (qtype == Q4_1 ? 3 : 1);
+}
+// Q4_1 weight sums, precomputed at repack: the AVX2 dot's `sums` term for the even
+// chains (ggml.c:2236-2240, _mm256_sad_epu8 of the weight bytes 8k..8k+7 = the nibbles
+// of qs[4k..4k+3], chain 2k) as one byte per block.  wsum[g][c][8r+j] (uint4): chain
+// 2(j/2) of row 8g+r, blocks 32c + 16(j%2) .. +15 of the chunk, byte t = block +t.
+inline const uint4 * q41_wsum(const QMatrix & w) {
+    return (const uint4 *) ((const char *) w.scl + (size_t) w.M * ((w.K / 32 + 31) / 32) * 256);
 }
 
 // prompt-eval (N > 1) Q4_0 matmul on the MFMA cores (mm_mfma.hip), bit-exact

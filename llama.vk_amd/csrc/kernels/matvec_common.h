@@ -160,7 +160,10 @@ __device__ __forceinline__ void q41_quad(const float v[8], float & d, float & m,
 //   act[nb/4][8] uint4 : {a(4u,j), a(4u+1,j) << 16, a(4u+2,j), a(4u+3,j) << 16}
 //   dyv, myv [NC][8][4] : d / m of block 32c + 8m + j at [c][j][m]
 //   ysum[nb/4][4 q][4]  : sum of the 8 nibbles 8q..8q+7 of block 4u+t at [u][q][t]
-__device__ __forceinline__ void act41_store(uint32_t * act, float * dyv, float * myv, float * ysum, int i,
+// ysum: float per (block, chain pair) for matvec_q41.hip; one byte each for
+// matvec_cu41.hip (the sums are integers <= 120), same index
+template <typename YS>
+__device__ __forceinline__ void act41_store(uint32_t * act, float * dyv, float * myv, YS * ysum, int i,
                                             const uint32_t qs[4], float d, float m) {
     const int slot = i & 3;
     const uint32_t sh = (slot & 1) ? 16u : 0u;
@@ -172,7 +175,7 @@ __device__ __forceinline__ void act41_store(uint32_t * act, float * dyv, float *
         base[j * 4 + slot] = (lo | (hi << 8)) << sh;
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) ysum[(size_t) (i >> 2) * 16 + q * 4 + slot] = (float) udot8(qs[q], 0x11111111u);
+    for (int q = 0; q < 4; ++q) ysum[(size_t) (i >> 2) * 16 + q * 4 + slot] = (YS) udot8(qs[q], 0x11111111u);
     const int o = (i >> 5) * 32 + (i & 7) * 4 + ((i >> 3) & 3);
     dyv[o] = d;
     myv[o] = m;

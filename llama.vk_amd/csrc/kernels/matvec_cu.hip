@@ -56,6 +56,11 @@ struct CuParams {
     const uint16_t * silu_tab;
 };
 
+// per-wave block-scale table s = dw * dx in LDS (two buffers, 8 rows x 32 blocks): the row
+// stride is padded to 40 floats so the rows start on banks 0, 40, 16, 56, 32, 8, 48, 24 of
+// the 64 and the per-row broadcast float4 reads are bank-conflict free
+constexpr int SRS = 40, SPL = 8 * SRS;
+
 template <int NW, int NP, int D, int PRO, int EPI, int KT>
 __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     constexpr int PT = NP * 64;                 // prologue threads
@@ -70,7 +75,7 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t * act = (uint32_t *) smem;                          // nb * 32 B
     float * dxp = (float *) (smem + nb * 32);                    // NC * 128 B
-    float * sbuf = dxp + NC * 32;                                // NW * 2 * 256 floats
+    float * sbuf = dxp + NC * 32;                                // NW * 2 * SPL floats
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -228,7 +233,7 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
 
     if constexpr (NP == 0) {
-        double * red = (double *) (sbuf + NW * 512);     // NW doubles (after the s buffers)
+        double * red = (double *) (sbuf + NW * 2 * SPL); // NW doubles (after the s buffers)
         if constexpr (FPRO) {
             float scale = 1.0f;
             if constexpr (PRO == PRO_NORM) {
@@ -299,7 +304,7 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     if (NP == 0 && ng == 0) return;
 
     // 4. row groups: chunk loop with cross-group prefetch
-    float * sw = sbuf + wave * 2 * 256;
+    float * sw = sbuf + wave * 2 * SPL;
     auto body = [&](auto has_next, int grp, int gnext) __attribute__((always_inline)) {
         float acc = 0.0f;
 #pragma unroll
@@ -312,17 +317,17 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
 #else
             {
 #endif
-            float * sl = sw + (c & 1) * 256;
+            float * sl = sw + (c & 1) * SPL;
             // s = dw * dx of blocks 32c + 8m + j of row r (ggml.c:1968)
             const float4 dx = *(const float4 *) (dxp + c * 32 + j * 4);
             float4 sv;
             sv.x = S[slot].x * dx.x; sv.y = S[slot].y * dx.y; sv.z = S[slot].z * dx.z; sv.w = S[slot].w * dx.w;
-            *(float4 *) (sl + r * 32 + j * 4) = sv;
+            *(float4 *) (sl + r * SRS + j * 4) = sv;
             __builtin_amdgcn_wave_barrier();
             float sa[8][4];
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
-                const float4 v = *(const float4 *) (sl + r * 32 + jj * 4);
+                const float4 v = *(const float4 *) (sl + r * SRS + jj * 4);
                 sa[jj][0] = v.x; sa[jj][1] = v.y; sa[jj][2] = v.z; sa[jj][3] = v.w;
             }
 #pragma unroll
@@ -415,7 +420,7 @@ hipError_t go(const CuParams & P, hipStream_t s) {
     const int nwg = std::min(cu_count(), P.G);
     // without cross-group prefetch every wave must own at most one group
     if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
-    const size_t lds = (size_t) nb * 32 + NC * 128 + NW * 2 * 1024 + NW * 8;
+    const size_t lds = (size_t) nb * 32 + NC * 128 + NW * 2 * SPL * 4 + NW * 8;
     LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
     return hipGetLastError();
 }

@@ -29,6 +29,7 @@ using namespace mv;
 struct Cu41Params {
     const uint4 * nib;
     const float4 * scl;         // [G][NC][2][64]: d, then m
+    const uint4 * wsum;         // [G][NC][64]: even-chain weight sums (lvk_kernels.h q41_wsum)
     int G;                      // row groups (M / 8)
     const float * x;            // PRO_NORM / PRO_ACTF: f32 input [K]
     const float * g;            // PRO_NORM: norm weight [K]
@@ -45,6 +46,12 @@ struct Cu41Params {
     const uint16_t * silu_tab;
 };
 
+// per-wave block-product tables in LDS: 4 tables (s, dx*my, mx*dy, mx*my) of 8 rows x 32
+// blocks; the row stride is padded to 40 floats so the 8 rows start on banks 0, 40, 16, 56,
+// 32, 8, 48, 24 (64 banks): the per-row broadcast float4 reads and the lane stores are
+// bank-conflict free (a 32-float stride put rows 0/2/4/6 on the same banks)
+constexpr int SRS = 40, SPL = 8 * SRS, SWF = 4 * SPL;
+
 template <int NW, int D, int PRO, int EPI, int KT>
 __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     constexpr int nb = KT / 32;                 // blocks per row
@@ -60,9 +67,9 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     uint32_t * act = (uint32_t *) smem;                          // nb * 32 B
     float * dyv = (float *) (smem + nb * 32);                    // NC * 32
     float * myv = dyv + NC * 32;                                 // NC * 32
-    float * ys = myv + NC * 32;                                  // nb * 4
-    float * sbuf = ys + nb * 4;                                  // NW * 1024
-    double * red = (double *) (sbuf + NW * 1024);                // NW
+    uint8_t * ys = (uint8_t *) (myv + NC * 32);                  // nb * 4 bytes: activation sums
+    float * sbuf = (float *) (ys + nb * 16);                     // NW * SWF (after nb * 4 floats of room)
+    double * red = (double *) (sbuf + NW * SWF);                 // NW
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -106,6 +113,7 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     // first D chunks of this wave's first row group (scalar-base loads)
     const uint32_t loff = ng > 0 ? (uint32_t) lane * 16u : 0u;
     uint4 W[D][4];
+    uint4 WS[D];
     float4 SD[D], SM[D];
 #define LVK_ISSUE41(slot, grp, cc)                                                                      \
     do {                                                                                                \
@@ -115,6 +123,7 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
         const char * sc_ = (const char *) (P.scl + ((size_t) (grp) * NC + (cc)) * 128) + loff;          \
         SD[slot] = *(const float4 *) sc_;                                                               \
         SM[slot] = *(const float4 *) (sc_ + 1024);                                                      \
+        WS[slot] = ld_nt((const uint4 *) ((const char *) (P.wsum + ((size_t) (grp) * NC + (cc)) * 64) + loff)); \
         __builtin_amdgcn_sched_barrier(0);                                                              \
     } while (0)
 #pragma unroll
@@ -185,9 +194,8 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
 
     // row groups: chunk loop with cross-group prefetch
     const bool even = (j & 1) == 0;
-    const bool other = (j == 2 || j == 4);
-    const uint32_t wsh = j >= 4 ? 8u : 0u;
-    float * sw = sbuf + wave * 1024;
+    const uint32_t * ys32 = (const uint32_t *) ys;
+    float * sw = sbuf + wave * SWF;
     auto body = [&](auto has_next, int grp, int gnext, float & off) __attribute__((always_inline)) {
         float acc = 0.0f;
         off = 0.0f;
@@ -199,7 +207,7 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
                 // s = dx*dy, ce = dx*my, co = mx*dy, mm = mx*my; slot 8m + j = block 32c + 8m + j
                 const float4 dy = *(const float4 *) (dyv + c * 32 + j * 4);
                 const float4 my = *(const float4 *) (myv + c * 32 + j * 4);
-                float * sl = sw + r * 32 + j;
+                float * sl = sw + r * SRS + j;
                 const float dxa[4] = {SD[slot].x, SD[slot].y, SD[slot].z, SD[slot].w};
                 const float mxa[4] = {SM[slot].x, SM[slot].y, SM[slot].z, SM[slot].w};
                 const float dya[4] = {dy.x, dy.y, dy.z, dy.w};
@@ -207,14 +215,23 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
 #pragma unroll
                 for (int mq = 0; mq < 4; ++mq) {
                     sl[mq * 8] = dxa[mq] * dya[mq];
-                    sl[256 + mq * 8] = dxa[mq] * mya[mq];
-                    sl[512 + mq * 8] = mxa[mq] * dya[mq];
-                    sl[768 + mq * 8] = mxa[mq] * mya[mq];
+                    sl[SPL + mq * 8] = dxa[mq] * mya[mq];
+                    sl[2 * SPL + mq * 8] = mxa[mq] * dya[mq];
+                    sl[3 * SPL + mq * 8] = mxa[mq] * mya[mq];
                 }
                 __builtin_amdgcn_wave_barrier();
-                const float * srow = sw + r * 32;
-                const float * xrow = srow + (even ? 256 : 512);
-                const float * mrow = srow + 768;
+                const float * srow = sw + r * SRS;
+                const float * xrow = srow + (even ? SPL : 2 * SPL);
+                const float * mrow = srow + 3 * SPL;
+                // the block sums multiplying the cross scales (ggml.c:2236-2240): even chains
+                // take the precomputed weight sums (blocks 0-15 of the chunk in their own word,
+                // 16-31 in the odd neighbour's: DPP quad_perm [1,1,3,3]), odd chains the
+                // activation sums from LDS; one byte per block, exact as floats
+                const uint32_t wown[4] = {WS[slot].x, WS[slot].y, WS[slot].z, WS[slot].w};
+                uint32_t wnb[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    wnb[q] = (uint32_t) __builtin_amdgcn_mov_dpp((int) wown[q], 0xF5, 0xF, 0xF, false);
 #pragma unroll
                 for (int sb = 0; sb < 4; ++sb) {
                     if (c * 4 + sb < nsub) {
@@ -227,11 +244,11 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
                             const float4 s4 = *(const float4 *) (srow + bi);
                             const float4 x4 = *(const float4 *) (xrow + bi);
                             const float4 m4 = *(const float4 *) (mrow + bi);
-                            const float4 y4 = *(const float4 *) (ys + (size_t) uu * 16 + (j >> 1) * 4);
-                            const uint32_t w01 = wsum_word(wd[2 * pp], other, wsh);
-                            const uint32_t w23 = wsum_word(wd[2 * pp + 1], other, wsh);
-                            const float S[4] = {even ? (float) (w01 & 0xFFFFu) : y4.x, even ? (float) (w01 >> 16) : y4.y,
-                                                even ? (float) (w23 & 0xFFFFu) : y4.z, even ? (float) (w23 >> 16) : y4.w};
+                            const uint32_t ydw = ys32[(size_t) uu * 4 + (j >> 1)];
+                            const uint32_t wdw = sb < 2 ? wown[(sb & 1) * 2 + pp] : wnb[(sb & 1) * 2 + pp];
+                            const uint32_t sdw = even ? wdw : ydw;
+                            const float S[4] = {(float) (sdw & 0xFFu), (float) ((sdw >> 8) & 0xFFu),
+                                                (float) ((sdw >> 16) & 0xFFu), (float) (sdw >> 24)};
                             const int p[4] = {udot8(wd[2 * pp], a.x), udot8(wd[2 * pp], a.y),
                                               udot8(wd[2 * pp + 1], a.z), udot8(wd[2 * pp + 1], a.w)};
                             const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
@@ -316,7 +333,7 @@ hipError_t go(const Cu41Params & P, hipStream_t s) {
     const int nwg = std::min(cu_count(), P.G);
     // without cross-group prefetch every wave must own at most one group
     if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
-    const size_t lds = (size_t) nb * 32 + 2 * NC * 128 + (size_t) nb * 16 + NW * 4096 + NW * 8;
+    const size_t lds = (size_t) nb * 32 + 2 * NC * 128 + (size_t) nb * 16 + NW * SWF * 4 + NW * 8;
     LVK_LAUNCH((k_mv_cu41<NW, D, PRO, EPI, KT>), dim3(nwg), dim3(NW * 64), lds, s, P);
     return hipGetLastError();
 }
@@ -330,6 +347,7 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
     Cu41Params P{};
     P.nib = L.w.nib;
     P.scl = (const float4 *) L.w.scl;
+    P.wsum = q41_wsum(L.w);
     P.G = L.w.M / 8;
     P.x = L.x ? L.x + (size_t) L.tok0 * L.w.K : nullptr;
     P.g = L.g;
@@ -346,23 +364,23 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
     P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx; P.kv32 = L.kv32;
     P.silu_tab = L.silu_tab;
     const int K = L.w.K;
-#ifdef LVK_PROBE_SWEEP   // dev probe builds only: LVK_CFG41 selects a launch shape
+#ifdef LVK_PROBE_SWEEP   // dev probe builds only: LVK_CFG41 selects a launch shape (waves, prefetch depth)
     {
         static int cfg = getenv("LVK_CFG41") ? atoi(getenv("LVK_CFG41")) : 0;
         if (K == 5120 && epi == EPI_QKV) {
-            if (cfg == 1) return go<8, 3, PRO_NORM, EPI_QKV, 5120>(P, s);
+            if (cfg == 1) return go<8, 1, PRO_NORM, EPI_QKV, 5120>(P, s);
             if (cfg == 2) return go<4, 5, PRO_NORM, EPI_QKV, 5120>(P, s);
-            if (cfg == 3) return go<16, 2, PRO_NORM, EPI_QKV, 5120>(P, s);
+            if (cfg == 3) return go<8, 5, PRO_NORM, EPI_QKV, 5120>(P, s);
         }
         if (K == 5120 && epi == EPI_SWIGLU_F32) {
-            if (cfg == 1) return go<8, 5, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
-            if (cfg == 2) return go<14, 3, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
-            if (cfg == 3) return go<16, 1, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
+            if (cfg == 1) return go<7, 5, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
+            if (cfg == 2) return go<8, 1, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
+            if (cfg == 3) return go<4, 5, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
         }
         if (K == 5120 && epi == EPI_RESID) {
             if (cfg == 1) return go<3, 5, PRO_ACTQ, EPI_RESID, 5120>(P, s);
-            if (cfg == 2) return go<4, 3, PRO_ACTQ, EPI_RESID, 5120>(P, s);
-            if (cfg == 3) return go<2, 5, PRO_ACTQ, EPI_RESID, 5120>(P, s);
+            if (cfg == 2) return go<3, 1, PRO_ACTQ, EPI_RESID, 5120>(P, s);
+            if (cfg == 3) return go<4, 2, PRO_ACTQ, EPI_RESID, 5120>(P, s);
         }
         if (K == 13824 && epi == EPI_RESID) {
             if (cfg == 1) return go<4, 7, PRO_ACTF, EPI_RESID, 13824>(P, s);
@@ -370,21 +388,25 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
             if (cfg == 3) return go<2, 7, PRO_ACTF, EPI_RESID, 13824>(P, s);
         }
         if (K == 5120 && epi == EPI_STORE && pro == PRO_NORM) {
-            if (cfg == 1) return go<8, 5, PRO_NORM, EPI_STORE, 5120>(P, s);
-            if (cfg == 2) return go<16, 1, PRO_NORM, EPI_STORE, 5120>(P, s);
+            if (cfg == 1) return go<8, 1, PRO_NORM, EPI_STORE, 5120>(P, s);
+            if (cfg == 2) return go<4, 5, PRO_NORM, EPI_STORE, 5120>(P, s);
+            if (cfg == 3) return go<6, 5, PRO_NORM, EPI_STORE, 5120>(P, s);
         }
     }
 #endif
-    // launch shapes per row length and role: waves such that every CU keeps ~60-120 KB
-    // of weights in flight (K = 5120: NC = 5 chunks per row, so D = 2 does not divide
-    // the row and every wave owns at most one 8-row group)
+    // launch shapes per row length and role (waves NW, chunks in flight per wave D): every
+    // CU keeps ~60-280 KB of weights in flight.  K = 5120 has NC = 5 chunks per row: D = 2
+    // does not divide the row (every wave owns at most one 8-row group, so W1|W3 and the
+    // lm_head would need 14-16 waves = 128 VGPRs, which spills); with 8 waves they prefetch
+    // across groups (D = 1: 190 VGPRs, no scratch; measured on 13B: W1|W3 25.2 us vs 27.9
+    // at D = 5 and 29.3 for 14 waves, lm_head 27.4 vs 30.1)
     if (K == 5120) {
         switch (epi) {
             case EPI_QKV: if (pro == PRO_NORM) return go<8, 2, PRO_NORM, EPI_QKV, 5120>(P, s); break;
-            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<14, 2, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s); break;
+            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<8, 1, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s); break;
             case EPI_STORE:
-                if (pro == PRO_NORM) return go<16, 2, PRO_NORM, EPI_STORE, 5120>(P, s);
-                if (pro == PRO_ACTF) return go<16, 2, PRO_ACTF, EPI_STORE, 5120>(P, s);
+                if (pro == PRO_NORM) return go<8, 1, PRO_NORM, EPI_STORE, 5120>(P, s);
+                if (pro == PRO_ACTF) return go<8, 1, PRO_ACTF, EPI_STORE, 5120>(P, s);
                 break;
             case EPI_RESID: if (pro == PRO_ACTQ) return go<3, 2, PRO_ACTQ, EPI_RESID, 5120>(P, s); break;
         }

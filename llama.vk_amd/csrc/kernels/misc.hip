@@ -117,6 +117,20 @@ __global__ void k_repack_q41(const uint8_t * __restrict__ src, int M, int K, uin
     }
     scl[(((size_t) g * NC + c) * 2) * 64 + lane] = make_float4(d[0], d[1], d[2], d[3]);
     scl[(((size_t) g * NC + c) * 2 + 1) * 64 + lane] = make_float4(m[0], m[1], m[2], m[3]);
+    // weight-sum image after the d/m images (lvk_kernels.h q41_wsum): lane (r, j) holds
+    // chain 2k = 2(j/2)'s sums of blocks 32c + 16(j%2) + t, t = 0..15, one byte each
+    const int k = j >> 1;
+    uint32_t ws[4] = {0u, 0u, 0u, 0u};
+    for (int t = 0; t < 16; ++t) {
+        const int i = 32 * c + 16 * (j & 1) + t;
+        if (i >= nb) break;
+        const uint8_t * q = rb + (size_t) i * 24 + 8 + 4 * k;
+        uint32_t sum = 0;
+        for (int e = 0; e < 4; ++e) sum += (q[e] & 15u) + (q[e] >> 4);
+        ws[t >> 2] |= sum << (8 * (t & 3));
+    }
+    uint4 * wsum = (uint4 *) (scl + (size_t) M * NC * 16);     // d + m: M * NC * 256 bytes
+    wsum[((size_t) g * NC + c) * 64 + lane] = make_uint4(ws[0], ws[1], ws[2], ws[3]);
 }
 
 // standalone Q4_1 activation quantizer (quantize_row_q4_1 AVX2, ggml.c:847-920),
