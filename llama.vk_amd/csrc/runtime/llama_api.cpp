@@ -313,8 +313,8 @@ static int env_split_micro() {
     return e ? std::max(0, atoi(e)) : 64;
 }
 
-// LVK_SEGV_TRACE=1 (diagnostics): a SIGSEGV prints the faulting address and the native
-// frames to stderr, then the default action runs (core dump / exit 139)
+// LVK_SEGV_TRACE=1 (diagnostics): a SIGSEGV / SIGBUS / SIGABRT prints the faulting address
+// and the native frames to stderr, then the default action runs (core dump / exit 139, 134)
 static void segv_trace(int sig, siginfo_t * si, void *) {
     char buf[96];
     const int n = snprintf(buf, sizeof(buf), "llama.vk_amd: signal %d at address %p; native frames:\n", sig,
@@ -334,6 +334,7 @@ static void maybe_install_segv_trace() {
     sa.sa_flags = SA_SIGINFO;
     sigaction(SIGSEGV, &sa, nullptr);
     sigaction(SIGBUS, &sa, nullptr);
+    sigaction(SIGABRT, &sa, nullptr);
 }
 
 struct llama_context * llama_init_from_file(const char * path_model, struct llama_context_params params) {

@@ -159,21 +159,48 @@ def test_split_shapes_vs_oracle(lvk, oracle, model_dir, cfg, stages, micro):
     om.close()
 
 
+STAGE_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, %(pkg)r)
+import lvk
+PROMPT = %(prompt)r
+path = %(model)r
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+ref = lvk.Llama(path, n_ctx=128)
+want = ref.eval(PROMPT, 0)
+tok, wt = int(np.argmax(want[-1])), []
+for i in range(10):
+    wt.append(tok)
+    tok = int(np.argmax(ref.eval([tok], len(PROMPT) + i)[-1]))
+wt.append(tok)
+ref.close()
+st = lvk.Llama(path, n_ctx=128, layers=(0, lvk.model_hparams(path)["n_layer"]))
+st.stage_connect(lvk.rccl_unique_id(), 1, 0)
+assert st.stage_step(PROMPT, len(PROMPT), 0, micro=7) == 0
+assert np.array_equal(bits(st.logits()[-1]), bits(want[-1]))
+tok, got = wt[0], [wt[0]]
+for i in range(10):
+    tok = st.stage_step([tok], 1, len(PROMPT) + i, greedy=True)
+    got.append(tok)
+assert got == wt, (got, wt)
+st.close()
+print("STAGE-LINK-OK", flush=True)
+"""
+
+
 def test_stage_link_single_rank(lvk, tiny_models):
     """the one-stage-per-process link (lvk_rccl_unique_id / lvk_stage_connect /
     lvk_stage_step, what bench.py's layer-split ranks run) with one rank: RCCL loads, the
-    communicator forms, and prompt micro-batches + greedy steps equal the plain context"""
-    path = tiny_models["tiny_q4_0"]
-    ref = lvk.Llama(path, n_ctx=128)
-    want, wt = run(ref, PROMPT, 10)
-    ref.close()
-    st = lvk.Llama(path, n_ctx=128, layers=(0, lvk.model_hparams(path)["n_layer"]))
-    st.stage_connect(lvk.rccl_unique_id(), 1, 0)
-    assert st.stage_step(PROMPT, len(PROMPT), 0, micro=7) == 0
-    assert np.array_equal(bits(st.logits()[-1]), bits(want[0][-1]))
-    tok, got = wt[0], [wt[0]]
-    for i in range(10):
-        tok = st.stage_step([tok], 1, len(PROMPT) + i, greedy=True)
-        got.append(tok)
-    assert got == wt
-    st.close()
+    communicator forms, and prompt micro-batches + greedy steps equal the plain context.
+    Runs in its own process, as each bench rank does: RCCL's state then lives and is torn
+    down with that process only, and the child must also exit cleanly (rc 0)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = STAGE_CHILD % {"pkg": os.path.join(root, "llama.vk_amd"), "prompt": PROMPT,
+                          "model": tiny_models["tiny_q4_0"]}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
+    assert "STAGE-LINK-OK" in r.stdout, r.stdout + r.stderr[-3000:]
+    assert r.returncode == 0, "stage-link child exited with %d: %s" % (r.returncode, r.stderr[-3000:])
