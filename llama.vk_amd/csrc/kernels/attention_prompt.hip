@@ -240,9 +240,9 @@ __global__ __launch_bounds__(256) void k_attn_p_pv(const uint16_t * __restrict__
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 hh[k] = __builtin_bit_cast(uint16_t, (_Float16) (float) ((int) ((word >> (4 * k)) & 15u) - 8));
-            uint2 * fr = xm + ((size_t) ((tok >> 4) * nb + blk) * 4 + e) * 64 + (tok & 15);
-            fr[0] = make_uint2(hh[0] | (uint32_t) hh[2] << 16, hh[1] | (uint32_t) hh[3] << 16);
-            fr[48] = make_uint2(hh[4] | (uint32_t) hh[6] << 16, hh[5] | (uint32_t) hh[7] << 16);
+            xm[xm_slot(tok, nb, blk, e, tok & 15)] = make_uint2(hh[0] | (uint32_t) hh[2] << 16, hh[1] | (uint32_t) hh[3] << 16);
+            xm[xm_slot(tok, nb, blk, e, 48 + (tok & 15))] =
+                make_uint2(hh[4] | (uint32_t) hh[6] << 16, hh[5] | (uint32_t) hh[7] << 16);
             if (e == 0) xda[(size_t) tok * nb + blk] = dd;
         }
     }

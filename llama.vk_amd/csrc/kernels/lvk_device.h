@@ -134,4 +134,13 @@ __device__ __forceinline__ float warp_max(float v) {
     return v;
 }
 
+// Masked B fragment image of the MFMA prompt matmul (mm_mfma.hip): token t, block b of nb,
+// chain pair c (chains 2c, 2c+1), fragment lane l.  The fragments of chain pairs 2q and 2q+1
+// sit side by side per lane, so a wave fetches two MFMA B operands with one 16-byte-per-lane
+// load (the texture unit's cost is per load instruction: 8-byte loads moved half the bytes
+// per cycle).  Returns the index in 8-byte units.
+__device__ __forceinline__ size_t xm_slot(int t, int nb, int b, int c, int l) {
+    return ((((size_t) (t >> 4) * nb + b) * 2 + (c >> 1)) * 64 + l) * 2 + (c & 1);
+}
+
 }  // namespace lvk

@@ -3,6 +3,7 @@
 // Every launcher is stream-ordered and capture-safe (no allocation, no sync),
 // so the decode step can be recorded into one hipGraph.
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <stdint.h>
@@ -57,6 +58,9 @@ struct QMatrix {
     int M = 0, K = 0;
     const uint4 * nib = nullptr;
     const void * scl = nullptr;
+    // optional f16 A-fragment image for the prompt matmul (launch_build_a16): 4x the
+    // weight bytes, saves the nibble unpack in k_mm_q40_mfma; nullptr = unpack path
+    const void * a16 = nullptr;
 };
 
 // Activation quantized to the weight format, stored split: d[N][nb] floats,
@@ -201,6 +205,15 @@ inline const uint4 * q41_wsum(const QMatrix & w) {
 // (fused W1|W3 image -> u = silu(w1 x) * (w3 x)).
 bool mm_mfma_supported(const QMatrix & w);
 size_t mm_act_bytes(int N, int K);
+// the f16 A-fragment image of a Q4_0 matrix (QMatrix::a16): bytes, and its build from the
+// matrix's octet image (M % 32 == 0)
+size_t mm_a16_bytes(int M, int K);
+hipError_t launch_build_a16(const QMatrix & w, void * a16, hipStream_t s);
+// LVK_PROMPT_A16=0 keeps the prompt matmul on the nibble image (no f16 A image)
+inline bool prompt_a16_env() {
+    const char * e = getenv("LVK_PROMPT_A16");
+    return !e || atoi(e) != 0;
+}
 hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, int N, float * y, int ldy,
                           int out_tok0, int epi, const uint16_t * silu_tab, hipStream_t s);
 // x[N][K] (rms_norm * g when g != nullptr) -> quantize_row_q4_0 -> xm, da

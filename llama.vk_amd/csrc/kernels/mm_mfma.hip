@@ -27,7 +27,7 @@
 //     in the chain order e0 e2 e1 e3.
 //   B (activations): Q4_0-quantized tokens as f16 values q-8, written by the
 //     activation quantizer straight into the masked fragment image
-//       xm[token tile][block][c][64 lanes] x 8 B
+//       xm[token tile][block][c/2][64 lanes][c%2] x 8 B   (lvk_device.h xm_slot)
 //     (lane (h, jj, n): chain 2c+h of token n when h == jj, else zero), so a
 //     wave loads each fragment with one coalesced global_load_dwordx2 -- no
 //     LDS staging and no barrier per K step; 2 blocks are kept in flight (a
@@ -64,6 +64,16 @@ constexpr int NT = 256;     // threads (4 waves)
 #define LVK_MM_PD 2
 #endif
 constexpr int PD = LVK_MM_PD;   // B blocks in flight per wave (ring size divides 8; 4 spills at 256 VGPRs)
+#ifndef LVK_MM_PDA
+#define LVK_MM_PDA 4
+#endif
+// A16 variant: A and B blocks in flight per wave.  4 + 4 measured fastest (7B 512-token
+// prompt 45.4 ms; 4 + 2: 47.7, 2 + 4: 50.7, nibble unpack path 47.3) although it leaves
+// 4-6 VGPRs in scratch at the 256-VGPR budget of two waves per SIMD
+constexpr int PDA = LVK_MM_PDA;
+#ifndef LVK_MM_PDB16
+#define LVK_MM_PDB16 4
+#endif
 
 constexpr int DWS = TM + 8;                         // padded row stride of the dw image (conflict-free stores)
 constexpr int DAS = TN + 1;                         // padded stride of the da image
@@ -76,6 +86,7 @@ constexpr int LDS_TOTAL = OFF_DA1 + LDS_DA;         // ~37 KiB
 struct MmParams {
     const uint4 * nib;
     const float4 * scl;
+    const uint2 * a16;       // A16 variant: f16 A-fragment image [M/32][nb][4][64] (QMatrix::a16)
     int M, K, nb, NC;
     const uint2 * xm;        // masked B fragment image [ntt][nb][4][64]
     const float * da;        // [N][nb]
@@ -116,7 +127,10 @@ __device__ __forceinline__ f32x16_t fake_mfma(half4_t a, half4_t b) {   // LVK_M
     return r;
 }
 
-template <int EPI>
+// A16: the A fragments come ready-made from the f16 image (one global_load_dwordx2 per
+// MFMA, ring of PD blocks like B) instead of the nibble octet image + unpack (5 VALU per
+// MFMA, a third of the loop's VALU work)
+template <int EPI, bool A16>
 __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x;
@@ -183,14 +197,27 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
             else A[c] = p[2 * c];
         }
     };
+    // A16: lane (rho, h) of wave w reads the fragment of rows m0 + 32w + rho, chain 2c + h
+    const uint4 * a16p = A16 ? (const uint4 *) P.a16 + (size_t) (m0 / 32 + w) * nb * 128 + lane : nullptr;
+    uint2 aq[A16 ? PDA : 1][4];
+    auto load_aq = [&](int blk, uint2 (&q)[4]) {
+#pragma unroll
+        for (int c2 = 0; c2 < 2; ++c2) {
+            const uint4 v = a16p[(size_t) blk * 128 + c2 * 64];
+            q[2 * c2] = make_uint2(v.x, v.y);
+            q[2 * c2 + 1] = make_uint2(v.z, v.w);
+        }
+    };
     // ---- B operand: masked fragments of this token tile, 4 per block ----
-    const uint2 * bp = P.xm + (size_t) tt * nb * 256 + lane;
-    uint2 bq[PD][4];
+    const uint4 * bp = (const uint4 *) P.xm + (size_t) tt * nb * 128 + lane;   // xm_slot pairs
+    constexpr int PB = A16 ? LVK_MM_PDB16 : PD;       // B blocks in flight
+    uint2 bq[PB][4];
     auto load_bq = [&](int blk, uint2 (&q)[4]) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (LVK_MM_EXP & 4) q[c] = make_uint2(blk, c);
-            else q[c] = bp[(size_t) blk * 256 + c * 64];
+        for (int c2 = 0; c2 < 2; ++c2) {
+            const uint4 v = (LVK_MM_EXP & 4) ? make_uint4(blk, c2, 0, 1) : bp[(size_t) blk * 128 + c2 * 64];
+            q[2 * c2] = make_uint2(v.x, v.y);
+            q[2 * c2 + 1] = make_uint2(v.z, v.w);
         }
     };
 
@@ -211,18 +238,23 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
 
     uint4 Anext[4];
     load_scales(0);
-    load_a(0, Anext);
+    if constexpr (A16) {
 #pragma unroll
-    for (int d = 0; d < PD; ++d) load_bq(min(d, nb - 1), bq[d]);
+        for (int d = 0; d < PDA; ++d) load_aq(min(d, nb - 1), aq[d]);
+    } else {
+        load_a(0, Anext);
+    }
+#pragma unroll
+    for (int d = 0; d < PB; ++d) load_bq(min(d, nb - 1), bq[d]);
     store_scales(0);
-    make_x(Anext);
+    if constexpr (!A16) make_x(Anext);
     __syncthreads();
 
     for (int u = 0; u < U; ++u) {
         const int ch = u >> 2;
         const bool chunk_last = (u & 3) == 3 || u == U - 1;
         const bool scales_next = chunk_last && u + 1 < U;
-        if (u + 1 < U) load_a(u + 1, Anext);
+        if (!A16 && u + 1 < U) load_a(u + 1, Anext);
         if (scales_next) load_scales(ch + 1);
         const float * wl = (const float *) (smem + ((ch & 1) ? OFF_DW1 : OFF_DW0));
         const float * dl = (const float *) (smem + ((ch & 1) ? OFF_DA1 : OFF_DA0));
@@ -237,7 +269,7 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
         for (int jb = 0; jb < 8; ++jb) {
             const int blk = 8 * u + jb;
             const uint32_t sel = (jb & 1) ? 0x0C030C02u : 0x0C010C00u;
-            uint2 (&bf)[4] = bq[jb % PD];
+            uint2 (&bf)[4] = bq[jb % PB];
             if ((jb & 1) == 0) {
                 const int jc = (u & 3) * 8 + jb + h;        // block of the chunk this lane half feeds
                 const float dwa = wl[jc * DWS + 32 * w + rho];
@@ -251,11 +283,16 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
             // chains of pair c (ggml.c:2013: acc_j = fmaf(d, P_j, acc_j))
             f32x16_t Pc[2];
 #define LVK_MFMA(a, b) ((LVK_MM_EXP & 2) ? fake_mfma(a, b) : __builtin_amdgcn_mfma_f32_32x32x8f16(a, b, (f32x16_t){}, 0, 0, 0))
-            Pc[0] = LVK_MFMA(unpack_chain(X[0][jb >> 1], sel), __builtin_bit_cast(half4_t, bf[0]));
+            uint2 (&af)[4] = aq[A16 ? jb % PDA : 0];
+            auto afrag = [&](int c) __attribute__((always_inline)) -> half4_t {
+                if constexpr (A16) return __builtin_bit_cast(half4_t, af[c]);
+                else return unpack_chain(X[c][jb >> 1], sel);
+            };
+            Pc[0] = LVK_MFMA(afrag(0), __builtin_bit_cast(half4_t, bf[0]));
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 if (c + 1 < 4)
-                    Pc[(c + 1) & 1] = LVK_MFMA(unpack_chain(X[c + 1][jb >> 1], sel), __builtin_bit_cast(half4_t, bf[c + 1]));
+                    Pc[(c + 1) & 1] = LVK_MFMA(afrag(c + 1), __builtin_bit_cast(half4_t, bf[c + 1]));
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     if (LVK_MM_EXP & 1) acc[c][i] += (i == 0 ? Pc[c & 1][0] + sc[0] : 0.0f);
@@ -263,12 +300,13 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
                 }
             }
             // refill this slot with block blk + PD (its MFMAs have read the old fragments)
-            load_bq(min(blk + PD, nb - 1), bf);
+            load_bq(min(blk + PB, nb - 1), bf);
+            if constexpr (A16) load_aq(min(blk + PDA, nb - 1), af);
             // block order pinned: unconstrained, hipcc hoists later blocks' MFMAs and spills
 #pragma unroll
             for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(acc[c]));
         }
-        if (u + 1 < U) make_x(Anext);
+        if (!A16 && u + 1 < U) make_x(Anext);
         if (scales_next) {
             store_scales(ch + 1);
             __syncthreads();            // chunk ch+1's scales visible; chunk ch-1's buffer free again
@@ -401,9 +439,9 @@ __global__ __launch_bounds__(256) void k_act_q40_f16(const float * __restrict__ 
             // masked fragment image: chain 2c -> lane n (h = jj = 0), chain 2c+1 -> lane 48 + n (h = jj = 1),
             // each in the order e0 e2 e1 e3
             const int nb = K / 32, c = u & 3;
-            uint2 * fr = xm + ((size_t) ((t >> 4) * nb + (u >> 2)) * 4 + c) * 64 + (t & 15);
-            fr[0] = make_uint2(h[0] | (uint32_t) h[2] << 16, h[1] | (uint32_t) h[3] << 16);
-            fr[48] = make_uint2(h[4] | (uint32_t) h[6] << 16, h[5] | (uint32_t) h[7] << 16);
+            xm[xm_slot(t, nb, u >> 2, c, t & 15)] = make_uint2(h[0] | (uint32_t) h[2] << 16, h[1] | (uint32_t) h[3] << 16);
+            xm[xm_slot(t, nb, u >> 2, c, 48 + (t & 15))] =
+                make_uint2(h[4] | (uint32_t) h[6] << 16, h[5] | (uint32_t) h[7] << 16);
             if ((u & 3) == 0) da[(size_t) t * (K / 32) + (u >> 2)] = d;
         }
     }
@@ -425,10 +463,9 @@ __global__ void k_actq_to_f16(ActQ q, int N, int K, uint2 * __restrict__ xm, flo
         const int qv = (int) ((word >> (4 * e)) & 15u);
         h[e] = __builtin_bit_cast(uint16_t, (_Float16) (float) (qv - 8));
     }
-    const long t = tb / nb, b = tb % nb;
-    uint2 * fr = xm + ((size_t) ((t >> 4) * nb + b) * 4 + c) * 64 + (t & 15);
-    fr[0] = make_uint2(h[0] | (uint32_t) h[2] << 16, h[1] | (uint32_t) h[3] << 16);
-    fr[48] = make_uint2(h[4] | (uint32_t) h[6] << 16, h[5] | (uint32_t) h[7] << 16);
+    const int t = (int) (tb / nb), b = (int) (tb % nb);
+    xm[xm_slot(t, nb, b, c, t & 15)] = make_uint2(h[0] | (uint32_t) h[2] << 16, h[1] | (uint32_t) h[3] << 16);
+    xm[xm_slot(t, nb, b, c, 48 + (t & 15))] = make_uint2(h[4] | (uint32_t) h[6] << 16, h[5] | (uint32_t) h[7] << 16);
     if (c == 0) da[tb] = q.d[tb];
 }
 
@@ -465,7 +502,39 @@ __global__ void k_rope_kv(const float * __restrict__ qkv, int N, int E, int hd, 
     }
 }
 
+// f16 A-fragment image of a Q4_0 octet image (QMatrix::a16): a16[M/32][nb][c/2][lane][c%2] x 8 B,
+// lane (rho, h) = row 32 rt + rho, chain 2c + h: its 4 elements as f16 (q - 8) in the
+// fragment order e0 e2 e1 e3 (the order the activation image uses).  One thread per
+// 8-byte fragment, read from the octet word that holds the chain (k_repack_q40 layout).
+__global__ void k_a16_from_octet(const uint4 * __restrict__ nib, int M, int K, uint2 * __restrict__ a16) {
+    const int nb = K / 32, NC = (nb + 31) / 32;
+    const long idx = (long) blockIdx.x * blockDim.x + threadIdx.x;     // ((rt * nb + b) * 4 + c) * 64 + lane
+    if (idx >= (long) (M / 32) * nb * 256) return;
+    const int lane = (int) (idx & 63), c = (int) ((idx >> 6) & 3);
+    const long rb = idx >> 8;
+    const int b = (int) (rb % nb), rt = (int) (rb / nb);
+    const int row = rt * 32 + (lane & 31), jc = 2 * c + (lane >> 5);
+    const uint4 v = nib[(((size_t) (row >> 3) * NC + (b >> 5)) * 4 + ((b & 31) >> 3)) * 64 + 8 * (row & 7) + jc];
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t t = ((wd[(b & 7) >> 1] >> (16 * (b & 1))) & 0xFFFFu) ^ 0x8888u;   // byte0: e0 e1, byte1: e2 e3
+    uint16_t hq[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hq[e] = __builtin_bit_cast(uint16_t, (_Float16) (float) ((int) ((t >> (4 * e)) & 15u) - 8));
+    // chain pairs 2q, 2q+1 side by side per lane (as xm_slot): one 16-byte load per 2 MFMAs
+    a16[((((size_t) rt * nb + b) * 2 + (c >> 1)) * 64 + lane) * 2 + (c & 1)] =
+        make_uint2(hq[0] | (uint32_t) hq[2] << 16, hq[1] | (uint32_t) hq[3] << 16);
+}
+
 }  // namespace
+
+size_t mm_a16_bytes(int M, int K) { return (size_t) (M / 32) * (K / 32) * 256 * 8; }
+
+hipError_t launch_build_a16(const QMatrix & w, void * a16, hipStream_t s) {
+    if (w.qtype != Q4_0 || w.M % 32 || w.K % 256) return hipErrorInvalidValue;
+    const long n = (long) (w.M / 32) * (w.K / 32) * 256;
+    LVK_LAUNCH(k_a16_from_octet, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, w.nib, w.M, w.K, (uint2 *) a16);
+    return hipGetLastError();
+}
 
 bool mm_mfma_supported(const QMatrix & w) {
     return w.qtype == Q4_0 && w.M % TM == 0 && w.K % 256 == 0;
@@ -481,13 +550,20 @@ hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, 
     P.M = w.M; P.K = w.K; P.nb = w.K / 32; P.NC = (P.nb + 31) / 32;
     P.xm = (const uint2 *) xm; P.da = da; P.N = N; P.ntt = (N + TN - 1) / TN;
     P.y = y; P.ldy = ldy; P.out_tok0 = out_tok0; P.silu_tab = silu_tab;
+    P.a16 = (const uint2 *) w.a16;
     const dim3 grid((w.M / TM) * P.ntt);
+#define LVK_MM_GO(E)                                                                      \
+    do {                                                                                  \
+        if (P.a16) LVK_LAUNCH((k_mm_q40_mfma<E, true>), grid, dim3(NT), LDS_TOTAL, s, P); \
+        else LVK_LAUNCH((k_mm_q40_mfma<E, false>), grid, dim3(NT), LDS_TOTAL, s, P);      \
+    } while (0)
     switch (epi) {
-        case EPI_STORE: LVK_LAUNCH(k_mm_q40_mfma<EPI_STORE>, grid, dim3(NT), LDS_TOTAL, s, P); break;
-        case EPI_RESID: LVK_LAUNCH(k_mm_q40_mfma<EPI_RESID>, grid, dim3(NT), LDS_TOTAL, s, P); break;
-        case EPI_SWIGLU_F32: LVK_LAUNCH(k_mm_q40_mfma<EPI_SWIGLU_F32>, grid, dim3(NT), LDS_TOTAL, s, P); break;
+        case EPI_STORE: LVK_MM_GO(EPI_STORE); break;
+        case EPI_RESID: LVK_MM_GO(EPI_RESID); break;
+        case EPI_SWIGLU_F32: LVK_MM_GO(EPI_SWIGLU_F32); break;
         default: return hipErrorInvalidValue;
     }
+#undef LVK_MM_GO
     return hipGetLastError();
 }
 

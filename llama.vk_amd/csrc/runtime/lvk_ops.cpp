@@ -151,6 +151,10 @@ int lvk_mul_mat_q_mfma(int type, const void * w, int m, int k, const float * g, 
         q.nib = (const uint4 *) dv.get(lvk::qimage_nib_bytes(m, k));
         q.scl = dv.get(lvk::qimage_scl_bytes(m, k, type));
         LVK_HIP(lvk::launch_repack(wd, type, m, k, (uint4 *) q.nib, (void *) q.scl, nullptr));
+        if (lvk::prompt_a16_env()) {       // the f16 A-fragment variant, as the model loader builds it
+            q.a16 = dv.get(lvk::mm_a16_bytes(m, k));
+            LVK_HIP(lvk::launch_build_a16(q, (void *) q.a16, nullptr));
+        }
         float * xd = dv.up(x, (size_t) n * k);
         const float * gd = g ? dv.up(g, (size_t) k) : nullptr;
         void * xh = dv.get(lvk::mm_act_bytes(n, k));

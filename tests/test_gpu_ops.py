@@ -188,11 +188,15 @@ def test_rms_norm_mul(lvk, oracle):
 # ---------------------------------------------------------------------------
 # MFMA prompt matmul (mm_mfma.hip): the matrix cores produce the per-chain
 # integer partials, the VALU runs the reference's fp32 chains -> bit-exact
-# against ggml_vec_dot_q4_0's AVX2 order, incl. the fused RMSNorm+quantize.
+# against ggml_vec_dot_q4_0's AVX2 order, incl. the fused RMSNorm+quantize.  Both A
+# operand sources: the f16 A-fragment image (default) and the nibble unpack
+# (LVK_PROMPT_A16=0).
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("a16", ["1", "0"])
 @pytest.mark.parametrize("m,k,n,norm", [(128, 256, 2, False), (256, 4096, 64, True), (128, 4096, 70, False),
                                         (128, 11008, 17, False), (384, 1024, 130, True), (128, 5120, 3, True)])
-def test_mul_mat_mfma_bit_exact(lvk, oracle, m, k, n, norm):
+def test_mul_mat_mfma_bit_exact(lvk, oracle, monkeypatch, m, k, n, norm, a16):
+    monkeypatch.setenv("LVK_PROMPT_A16", a16)
     rng = np.random.default_rng(m + 3 * k + 11 * n)
     wq = _weights(oracle, rng, m, k, 2)
     x = (rng.standard_normal((n, k)) * 1.7).astype(np.float32)

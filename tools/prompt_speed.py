@@ -1,0 +1,37 @@
+"""Dev tool: 7B 512-token prompt eval time (best of 3) and per-kernel-class milliseconds, plus
+a hash of the last logits row (equal hashes across LVK_PROMPT_A16=0/1 = identical bits).
+usage: prompt_speed.py [n_tokens]"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'llama.vk_amd'))
+import numpy as np
+import lvk
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+path = '/tmp/lvk_bench/llama-7b-q4_0.bin'
+if not os.path.exists(path):
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    lvk.gen_model(path, vocab=os.path.join(ROOT, 'tests', 'golden', 'vocab32000.bin'),
+                  n_embd=4096, n_head=32, n_layer=32, ftype=2, seed=1)
+m = lvk.Llama(path, n_ctx=512)
+toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, n)], np.int32)
+best = 1e30
+for _ in range(3):
+    t0 = time.perf_counter()
+    lg = m.eval(toks, 0)
+    best = min(best, time.perf_counter() - t0)
+h = hashlib.sha1(np.ascontiguousarray(lg[-1]).tobytes()).hexdigest()[:16]
+m.set_profiling(True)
+m.reset_profile()
+m.eval(toks, 0)
+p = m.profile()
+m.set_profiling(False)
+m.close()
+print(json.dumps({'a16': os.environ.get('LVK_PROMPT_A16', '1'), 'n': n, 'ms': round(best * 1e3, 2),
+                  'tok_s': round(n / best, 1), 'logits_sha1': h,
+                  'kernels_ms': {k: round(v['ms'], 3) for k, v in p.items() if v['launches']}}), flush=True)
