@@ -40,13 +40,13 @@ LVK_API int lvk_mul_mat_q(int type, const void * w, int m, int k, const float * 
 LVK_API int lvk_mul_mat_q_norm(int type, const void * w, int m, int k, const float * g, const float * x, int n,
                                float * y);
 
-/* The prompt-batch (N > 1) matmul on the MFMA cores (mm_mfma.hip), Q4_0 only:
- * same inputs and meaning as lvk_mul_mat_q / lvk_mul_mat_q_norm (g != NULL:
- * fused RMSNorm * g), and the same result bits: the matrix cores produce each
- * AVX2 chain's exact 4-element integer partial and the f32 scale products
- * dw*dx (one rounding each), and the VALU runs the reference's 8 fp32 chains
- * and horizontal order (ggml.c:1950-2026).  Needs m % 128 == 0, k % 256 == 0,
- * n >= 1. */
+/* The prompt-batch (N > 1) matmul on the MFMA cores (mm_mfma.hip for Q4_0,
+ * mm_mfma41.hip for Q4_1): same inputs and meaning as lvk_mul_mat_q /
+ * lvk_mul_mat_q_norm (g != NULL: fused RMSNorm * g), and the same result bits:
+ * the matrix cores produce each AVX2 chain's exact 4-element integer partial
+ * (Q4_1 also the exact cross-term sums) and the f32 scale products (one rounding
+ * each), and the VALU runs the reference's 8 fp32 chains and horizontal order
+ * (ggml.c:1950-2026 / 2188-2258).  Needs m % 128 == 0, k % 256 == 0, n >= 1. */
 LVK_API int lvk_mul_mat_q_mfma(int type, const void * w, int m, int k, const float * g, const float * x, int n,
                                float * y);
 

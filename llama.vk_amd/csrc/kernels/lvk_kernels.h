@@ -61,6 +61,9 @@ struct QMatrix {
     // optional f16 A-fragment image for the prompt matmul (launch_build_a16): 4x the
     // weight bytes, saves the nibble unpack in k_mm_q40_mfma; nullptr = unpack path
     const void * a16 = nullptr;
+    // Q4_1 only: the prompt matmul's per-block side image (launch_build_mm41: weight
+    // sums + d / m per lane); with a16 it enables the Q4_1 MFMA path (mm_mfma41.hip)
+    const void * side = nullptr;
 };
 
 // Activation quantized to the weight format, stored split: d[N][nb] floats,
@@ -219,6 +222,20 @@ hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, 
 // x[N][K] (rms_norm * g when g != nullptr) -> quantize_row_q4_0 -> xm, da
 hipError_t launch_act_f16(const float * x, const float * g, int N, int K, void * xm, float * da, hipStream_t s);
 hipError_t launch_actq_to_f16(const ActQ & q, int N, int K, void * xm, float * da, hipStream_t s);
+// the Q4_1 prompt matmul (mm_mfma41.hip), bit-exact like launch_matvec: the matrix
+// cores produce the chain partials, the cross-term sums and the scale products, the
+// VALU runs ggml_vec_dot_q4_1's fp32 chains.  Weights: QMatrix::a16 (mm_a16_bytes, f16
+// q values) + QMatrix::side (mm41_side_bytes), both from launch_build_mm41.  Tokens: the
+// masked fragment image xm (mm_act_bytes, ZEROED once at allocation) + the side image
+// xs (mm41_act_side_bytes), from launch_act41_f16 / launch_actq41_to_f16.
+size_t mm41_side_bytes(int M, int K);
+size_t mm41_act_side_bytes(int N, int K);
+hipError_t launch_build_mm41(const QMatrix & w, void * a16, void * side, hipStream_t s);
+bool mm_mfma41_supported(const QMatrix & w);
+hipError_t launch_mm_mfma41(const QMatrix & w, const void * xm, const void * xs, int N, float * y, int ldy, int epi,
+                            const uint16_t * silu_tab, hipStream_t s);
+hipError_t launch_act41_f16(const float * x, const float * g, int N, int K, void * xm, void * xs, hipStream_t s);
+hipError_t launch_actq41_to_f16(const ActQ & q, int N, int K, void * xm, void * xs, hipStream_t s);
 // RoPE + KV append of stored Q|K|V rows qkv [N][3E]
 hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 * rope, const StepParams * sp,
                           int n_ctx, uint16_t * q16, uint16_t * kc, uint16_t * vc, hipStream_t s, int kv32 = 0);

@@ -537,6 +537,7 @@ hipError_t launch_build_a16(const QMatrix & w, void * a16, hipStream_t s) {
 }
 
 bool mm_mfma_supported(const QMatrix & w) {
+    if (w.qtype == Q4_1) return mm_mfma41_supported(w);
     return w.qtype == Q4_0 && w.M % TM == 0 && w.K % 256 == 0;
 }
 
@@ -544,7 +545,7 @@ size_t mm_act_bytes(int N, int K) { return (size_t) ((N + TN - 1) / TN) * (K / 3
 
 hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, int N, float * y, int ldy,
                           int out_tok0, int epi, const uint16_t * silu_tab, hipStream_t s) {
-    if (!mm_mfma_supported(w) || N <= 0) return hipErrorInvalidValue;
+    if (w.qtype != Q4_0 || !mm_mfma_supported(w) || N <= 0) return hipErrorInvalidValue;
     MmParams P{};
     P.nib = w.nib; P.scl = (const float4 *) w.scl;
     P.M = w.M; P.K = w.K; P.nb = w.K / 32; P.NC = (P.nb + 31) / 32;

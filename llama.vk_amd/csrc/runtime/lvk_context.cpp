@@ -112,6 +112,7 @@ void Context::init(const llama_context_params & p) {
         xh = (uint16_t *) model.alloc(mm_act_bytes((int) Cp, (int) KX));
         LVK_HIP(hipMemset(xh, 0, mm_act_bytes((int) Cp, (int) KX)));   // masked slots stay zero
         xda = (float *) model.alloc(Cp * (KX / 32) * 4);
+        if (model.qtype == Q4_1) xside = model.alloc(mm41_act_side_bytes((int) Cp, (int) KX));
         qkv32 = (float *) model.alloc(C * 3 * E * 4);
         uf = (float *) model.alloc(C * F * 4);
         prompt_exact = getenv("LVK_PROMPT_EXACT") && atoi(getenv("LVK_PROMPT_EXACT")) != 0;
@@ -289,7 +290,7 @@ static hipError_t mv_launch(const MvLaunch & L, int pro, int epi, hipStream_t s)
 // prompt batches go through the MFMA matmuls when every matrix of the model fits them
 bool Context::use_mfma(int n) const {
     // below 16 tokens the per-row VALU kernels win (the MFMA tile is 16 tokens wide)
-    if (n < 16 || prompt_exact || model.qtype != Q4_0) return false;
+    if (n < 16 || prompt_exact) return false;
     for (const Layer & ly : model.layers)
         if (!mm_mfma_supported(ly.wqkv) || !mm_mfma_supported(ly.wo) || !mm_mfma_supported(ly.w13) ||
             !mm_mfma_supported(ly.w2))
@@ -306,16 +307,23 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
         // prompt batch on the matrix cores: per layer
         //   act(norm) -> QKV (store) -> RoPE + KV append -> attention -> act -> Wo (+x)
         //   act(norm) -> W1|W3 (silu * mul) -> act -> W2 (+x)
+        // Q4_0: mm_mfma.hip (activation scales da); Q4_1: mm_mfma41.hip (side image xs)
+        const bool q41 = model.qtype == Q4_1;
+        auto act = [&](const float * xin, const float * g, int K) {
+            return q41 ? launch_act41_f16(xin, g, n, K, xh, xside, stream) : launch_act_f16(xin, g, n, K, xh, xda, stream);
+        };
+        auto mm = [&](const QMatrix & w, float * y, int ldy, int epi, const uint16_t * st) {
+            return q41 ? launch_mm_mfma41(w, xh, xside, n, y, ldy, epi, st, stream)
+                       : launch_mm_mfma(w, xh, xda, n, y, ldy, 0, epi, st, stream);
+        };
         if (model.has_embed)
             timed_launch(K_EMBED, 0, [&] { return launch_embed(model.tok_emb, model.emb_type, E, tok_src, n, x, stream); });
         for (size_t il = 0; il < model.layers.size(); ++il) {
             const Layer & ly = model.layers[il];
             uint16_t * kcl = kc_layer(il);
             uint16_t * vcl = vc_layer(il);
-            timed_launch(K_QKV, 0, [&] { return launch_act_f16(x, ly.attn_norm, n, E, xh, xda, stream); });
-            timed_launch(K_QKV, qbytes(ly.wqkv), [&] {
-                return launch_mm_mfma(ly.wqkv, xh, xda, n, qkv32, 3 * E, 0, EPI_STORE, nullptr, stream);
-            });
+            timed_launch(K_QKV, 0, [&] { return act(x, ly.attn_norm, E); });
+            timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mm(ly.wqkv, qkv32, 3 * E, EPI_STORE, nullptr); });
             timed_launch(K_QKV, 0, [&] {
                 return launch_rope_kv(qkv32, n, E, hd, rope, sp_d, n_ctx, q16, kcl, vcl, stream, kv32);
             });
@@ -323,26 +331,23 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
             at.exp_computed = exp_computed;
             at.err = err_d;
             at.kv32 = kv32;
-            if (!kv32 && attention_prompt_supported(E, H, n_ctx)) {
+            if (!q41 && !kv32 && attention_prompt_supported(E, H, n_ctx)) {
                 // writes the Wo input in both forms (ActQ and the MFMA fragment image)
                 timed_launch(K_ATTN, 0, [&] {
                     return launch_attention_prompt(at, (uint16_t *) scores, xh, xda, stream);
                 });
             } else {
                 timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
-                timed_launch(K_WO, 0, [&] { return launch_actq_to_f16(aq_attn, n, E, xh, xda, stream); });
+                timed_launch(K_WO, 0, [&] {
+                    return q41 ? launch_actq41_to_f16(aq_attn, n, E, xh, xside, stream)
+                               : launch_actq_to_f16(aq_attn, n, E, xh, xda, stream);
+                });
             }
-            timed_launch(K_WO, qbytes(ly.wo), [&] {
-                return launch_mm_mfma(ly.wo, xh, xda, n, x, E, 0, EPI_RESID, nullptr, stream);
-            });
-            timed_launch(K_W13, 0, [&] { return launch_act_f16(x, ly.ffn_norm, n, E, xh, xda, stream); });
-            timed_launch(K_W13, qbytes(ly.w13), [&] {
-                return launch_mm_mfma(ly.w13, xh, xda, n, uf, F, 0, EPI_SWIGLU_F32, silu_tab, stream);
-            });
-            timed_launch(K_W2, 0, [&] { return launch_act_f16(uf, nullptr, n, F, xh, xda, stream); });
-            timed_launch(K_W2, qbytes(ly.w2), [&] {
-                return launch_mm_mfma(ly.w2, xh, xda, n, x, E, 0, EPI_RESID, nullptr, stream);
-            });
+            timed_launch(K_WO, qbytes(ly.wo), [&] { return mm(ly.wo, x, E, EPI_RESID, nullptr); });
+            timed_launch(K_W13, 0, [&] { return act(x, ly.ffn_norm, E); });
+            timed_launch(K_W13, qbytes(ly.w13), [&] { return mm(ly.w13, uf, F, EPI_SWIGLU_F32, silu_tab); });
+            timed_launch(K_W2, 0, [&] { return act(uf, nullptr, F); });
+            timed_launch(K_W2, qbytes(ly.w2), [&] { return mm(ly.w2, x, E, EPI_RESID, nullptr); });
         }
         if (!model.has_head || !head) return;
         if (last_only || !mm_mfma_supported(model.output)) {
@@ -352,10 +357,9 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
             o.n_tokens = last_only ? 1 : n;
             timed_launch(K_LMHEAD, qbytes(model.output), [&] { return mv_launch(o, PRO_NORM, EPI_STORE, stream); });
         } else {
-            timed_launch(K_LMHEAD, 0, [&] { return launch_act_f16(x, model.norm, n, E, xh, xda, stream); });
+            timed_launch(K_LMHEAD, 0, [&] { return act(x, model.norm, E); });
             timed_launch(K_LMHEAD, qbytes(model.output), [&] {
-                return launch_mm_mfma(model.output, xh, xda, n, logits_out, (int) hp.n_vocab, 0, EPI_STORE, nullptr,
-                                      stream);
+                return mm(model.output, logits_out, (int) hp.n_vocab, EPI_STORE, nullptr);
             });
         }
         if (want_embedding)

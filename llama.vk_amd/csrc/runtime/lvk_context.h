@@ -105,6 +105,7 @@ struct Context {
     void * attn_gran = nullptr;  // [H][n_ctx] {tag, score} granules of the decode attention  // env LVK_ATTN_V1=1: single-token evals on the one-kernel attention.hip
     uint16_t * xh = nullptr;     // masked MFMA B-fragment image of the quantized activations (mm_act_bytes)
     float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales
+    void * xside = nullptr;      // Q4_1: the activations' side image (mm41_act_side_bytes)
     float * qkv32 = nullptr;     // [C][3E] Q|K|V rows before RoPE
     float * uf = nullptr;        // [C][F] silu(w1 x) * (w3 x)
 

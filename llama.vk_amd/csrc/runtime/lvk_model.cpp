@@ -270,20 +270,28 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
     };
     // the prompt matmul's f16 A-fragment images (mm_mfma.hip, 2 B per weight: 13.4 GB for
     // 7B, 130 GB for 65B): built when they fit next to the Q4 images with 8 GiB to spare
-    bool a16 = m.qtype == Q4_0 && prompt_a16_env();
+    // Q4_1: the f16 image plus the per-block side image (mm_mfma41.hip, 3 B per weight in
+    // all) are what the Q4_1 MFMA prompt path runs on; without them its prompts stay on the
+    // VALU kernels
+    bool a16 = prompt_a16_env();
     if (a16) {
         const size_t EE = (size_t) E * E, EF = (size_t) E * F;
-        const size_t need = 2 * ((4 * EE + 3 * EF) * (size_t) LN + (m.has_head ? (size_t) V * E : 0));
+        const size_t per_w = m.qtype == Q4_0 ? 2 : 3;
+        const size_t need = per_w * ((4 * EE + 3 * EF) * (size_t) LN + (m.has_head ? (size_t) V * E : 0));
         size_t free_b = 0, total_b = 0;
         LVK_HIP(hipMemGetInfo(&free_b, &total_b));
-        const size_t q4 = (size_t) ((double) need / 2 * 20.0 / 32.0);
+        const size_t q4 = (size_t) ((double) need / per_w * (m.qtype == Q4_0 ? 20.0 : 24.0) / 32.0);
         a16 = free_b > need + q4 + ((size_t) 8 << 30);
     }
     auto repack = [&](QMatrix & q, int interleave4 = 0) {
         LVK_HIP(launch_repack(stage, q.qtype, q.M, q.K, (uint4 *) q.nib, (void *) q.scl, s, interleave4));
-        if (a16 && mm_mfma_supported(q)) {
+        if (a16 && q.qtype == Q4_0 && mm_mfma_supported(q)) {
             q.a16 = m.alloc(mm_a16_bytes(q.M, q.K));
             LVK_HIP(launch_build_a16(q, (void *) q.a16, s));
+        } else if (a16 && q.qtype == Q4_1 && q.M % 128 == 0 && q.K % 256 == 0) {
+            q.a16 = m.alloc(mm_a16_bytes(q.M, q.K));
+            q.side = m.alloc(mm41_side_bytes(q.M, q.K));
+            LVK_HIP(launch_build_mm41(q, (void *) q.a16, (void *) q.side, s));
         }
         LVK_HIP(hipStreamSynchronize(s));
     };

@@ -141,17 +141,21 @@ int lvk_mul_mat_q_norm(int type, const void * w, int m, int k, const float * g, 
 
 int lvk_mul_mat_q_mfma(int type, const void * w, int m, int k, const float * g, const float * x, int n, float * y) {
     try {
-        if (type != lvk::Q4_0) return fail(__func__, "Q4_0 only");
+        if (type != lvk::Q4_0 && type != lvk::Q4_1) return fail(__func__, "Q4_0 / Q4_1 only");
         if (m % 128 || k % 256 || n < 1) return fail(__func__, "need m % 128 == 0, k % 256 == 0, n >= 1");
         Dev dv;
         const size_t nb = (size_t) k / 32;
-        void * wd = dv.up((const uint8_t *) w, (size_t) m * nb * 20);
+        void * wd = dv.up((const uint8_t *) w, (size_t) m * nb * (type == lvk::Q4_0 ? 20 : 24));
         lvk::QMatrix q;
         q.qtype = type; q.M = m; q.K = k;
         q.nib = (const uint4 *) dv.get(lvk::qimage_nib_bytes(m, k));
         q.scl = dv.get(lvk::qimage_scl_bytes(m, k, type));
         LVK_HIP(lvk::launch_repack(wd, type, m, k, (uint4 *) q.nib, (void *) q.scl, nullptr));
-        if (lvk::prompt_a16_env()) {       // the f16 A-fragment variant, as the model loader builds it
+        if (type == lvk::Q4_1) {            // the Q4_1 path always runs on its f16 + side images
+            q.a16 = dv.get(lvk::mm_a16_bytes(m, k));
+            q.side = dv.get(lvk::mm41_side_bytes(m, k));
+            LVK_HIP(lvk::launch_build_mm41(q, (void *) q.a16, (void *) q.side, nullptr));
+        } else if (lvk::prompt_a16_env()) {  // the f16 A-fragment variant, as the model loader builds it
             q.a16 = dv.get(lvk::mm_a16_bytes(m, k));
             LVK_HIP(lvk::launch_build_a16(q, (void *) q.a16, nullptr));
         }
@@ -159,10 +163,16 @@ int lvk_mul_mat_q_mfma(int type, const void * w, int m, int k, const float * g, 
         const float * gd = g ? dv.up(g, (size_t) k) : nullptr;
         void * xh = dv.get(lvk::mm_act_bytes(n, k));
         LVK_HIP(hipMemset(xh, 0, lvk::mm_act_bytes(n, k)));
-        float * da = (float *) dv.get((size_t) n * nb * 4);
         float * yd = (float *) dv.get((size_t) n * m * 4);
-        LVK_HIP(lvk::launch_act_f16(xd, gd, n, k, xh, da, nullptr));
-        LVK_HIP(lvk::launch_mm_mfma(q, xh, da, n, yd, m, 0, lvk::EPI_STORE, nullptr, nullptr));
+        if (type == lvk::Q4_1) {
+            void * xs = dv.get(lvk::mm41_act_side_bytes(n, k));
+            LVK_HIP(lvk::launch_act41_f16(xd, gd, n, k, xh, xs, nullptr));
+            LVK_HIP(lvk::launch_mm_mfma41(q, xh, xs, n, yd, m, lvk::EPI_STORE, nullptr, nullptr));
+        } else {
+            float * da = (float *) dv.get((size_t) n * nb * 4);
+            LVK_HIP(lvk::launch_act_f16(xd, gd, n, k, xh, da, nullptr));
+            LVK_HIP(lvk::launch_mm_mfma(q, xh, da, n, yd, m, 0, lvk::EPI_STORE, nullptr, nullptr));
+        }
         LVK_HIP(hipMemcpy(y, yd, (size_t) n * m * 4, hipMemcpyDeviceToHost));
         return 0;
     } catch (const lvk::Error & e) { return fail(__func__, e.msg); }

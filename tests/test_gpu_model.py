@@ -202,7 +202,7 @@ def test_mfma_prompt_tiny_logits_all_vs_oracle(lvk, oracle, tiny_models):
     om.close()
 
 
-@pytest.mark.parametrize("name", ["tiny_q4_0"])
+@pytest.mark.parametrize("name", ["tiny_q4_0", "tiny_q4_1"])
 def test_mfma_prompt_chunks_match_reference_golden(lvk, tiny_models, name):
     """the reference's chunking (prompt batches 16, 8, 24, then decode) with MFMA prompt batches,
     against the logits the reference build produced"""
@@ -230,6 +230,34 @@ def test_mfma_prompt_7b_shaped_vs_oracle(lvk, oracle, model_dir, monkeypatch, a1
     om = oracle.model(path, 512)
     toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 200)], np.int32)
     a = m.eval(toks, 0)
+    b = om.eval(toks, 0)
+    assert np.array_equal(bits(a), bits(b))
+    n_past, tok = len(toks), int(np.argmax(b[-1]))
+    for _ in range(4):
+        a = m.eval([tok], n_past)
+        b = om.eval([tok], n_past)
+        assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past
+        n_past += 1
+        tok = int(np.argmax(b[-1]))
+    m.close()
+    om.close()
+
+
+def test_mfma_prompt_13b_q4_1_shaped_vs_oracle(lvk, oracle, model_dir):
+    """LLaMA-13B layer shapes in Q4_1 (K = 5120 / 13824, 40 heads), 2 layers: a 100-token
+    prompt (ragged token tile) through the Q4_1 MFMA matmuls (mm_mfma41.hip), then decode on
+    the KV cache it wrote, bit-exact against the oracle"""
+    from oracle_lib import gen_model
+    path = gen_model(os.path.join(model_dir, "w5120_l2_q41.bin"), n_embd=5120, n_head=40, n_layer=2, ftype=3, seed=11)
+    m = lvk.Llama(path, n_ctx=256)
+    om = oracle.model(path, 256)
+    toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 100)], np.int32)
+    m.set_profiling(True)
+    m.reset_profile()
+    a = m.eval(toks, 0)
+    # the MFMA path ran: activation image, matmul and RoPE/KV launches in the QKV class per layer
+    assert m.profile()["qkv"]["launches"] == 6
+    m.set_profiling(False)
     b = om.eval(toks, 0)
     assert np.array_equal(bits(a), bits(b))
     n_past, tok = len(toks), int(np.argmax(b[-1]))

@@ -212,6 +212,32 @@ def test_mul_mat_mfma_bit_exact(lvk, oracle, monkeypatch, m, k, n, norm, a16):
     assert np.array_equal(bits(got), bits(want))
 
 
+# the Q4_1 MFMA matmul (mm_mfma41.hip): chain partials, cross-term sums and scale
+# products on the matrix cores, ggml_vec_dot_q4_1's chains on the VALU -> bit-exact.
+# Shapes: LLaMA-13B rows (K 5120 / 13824), ragged token tiles, a 130-token batch; blocks
+# with d = 0 (all-zero and constant activations, constant weight blocks).
+@pytest.mark.parametrize("m,k,n,norm", [(128, 256, 2, False), (256, 5120, 40, True), (128, 13824, 17, False),
+                                        (384, 1024, 130, True), (128, 4096, 16, False), (128, 5120, 3, True)])
+def test_mul_mat_mfma_q4_1_bit_exact(lvk, oracle, m, k, n, norm):
+    rng = np.random.default_rng(7 * m + k + 13 * n)
+    w = (rng.standard_normal((m, k)) * 0.02).astype(np.float32)
+    w[1, 32:64] = 0.01                                # a constant weight block (d = 0, m = 0.01)
+    w[2, :32] = 0.0                                   # an all-zero weight block
+    wq = np.stack([oracle.quantize(r, 3, reference=True) for r in w])
+    x = (rng.standard_normal((n, k)) * 1.7).astype(np.float32)
+    x[0, :32] = 0.0                                   # an all-zero activation block
+    x[-1, 64:96] = -0.5                               # a constant activation block
+    g = (1.0 + 0.1 * rng.standard_normal(k)).astype(np.float32) if norm else None
+    got = lvk.mul_mat_q_mfma(3, wq, m, k, x, g=g)
+    xin = x
+    if norm:
+        xn = np.zeros_like(x)
+        oracle.lib.orc_rms_norm(x, k, n, xn)
+        xin = (g[None, :] * xn).astype(np.float32)
+    want = _oracle_mm(oracle, wq, [oracle.quantize(r, 3) for r in xin], k, 3)
+    assert np.array_equal(bits(got), bits(want))
+
+
 # ---------------------------------------------------------------------------
 # the reference's op-level codec table (ggml.h:803-814) exported by this library
 # ---------------------------------------------------------------------------
