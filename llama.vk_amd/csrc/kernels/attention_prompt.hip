@@ -19,6 +19,7 @@
 //                    (ggml.c:621-685) fused, written as the Wo input (ActQ and,
 //                    for the MFMA Wo, the masked fragment image).
 #include "lvk_device.h"
+#include "mm41_common.h"
 #include "lvk_kernels.h"
 #include "matvec_common.h"
 
@@ -130,7 +131,8 @@ __global__ __launch_bounds__(256) void k_attn_p_scores(const uint16_t * __restri
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_attn_p_pv(const uint16_t * __restrict__ vc, const uint16_t * __restrict__ P,
                                                    const StepParams * sp, int E, int n_ctx, ActQ out, uint2 * xm,
-                                                   float * xda, float * __restrict__ out_f32) {
+                                                   float * xda, float * __restrict__ out_f32, int q41,
+                                                   uint4 * xs41) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int n_past = sp->n_past, N = sp->n_tokens;
     const int n_kv = n_past + N;
@@ -216,6 +218,25 @@ __global__ __launch_bounds__(256) void k_attn_p_pv(const uint16_t * __restrict__
         const float v = ob[t * 33 + e];
         const int tok = t0 + t;
         if (out_f32) out_f32[(size_t) tok * E + d0 + e] = v;
+        if (q41) {
+            // Q4_1 model: quantize_row_q4_1 (AVX2, ggml.c:847-920) of the block by the lane
+            // quad e < 4, written as the ActQ and (xs41 given) the Q4_1 MFMA operands (mm_mfma41.hip)
+            if (e < 4) {
+                float dd, mm;
+                uint32_t qword;
+                mv::q41_block_lds(ob + t * 33, e, dd, mm, qword);
+                const int base = (tid & 63) & ~3;
+                const uint32_t q0 = __shfl(qword, base), q1 = __shfl(qword, base + 1);
+                const uint32_t q2 = __shfl(qword, base + 2), q3 = __shfl(qword, base + 3);
+                if (e == 0) {
+                    out.d[(size_t) tok * out.nb + blk] = dd;
+                    out.m[(size_t) tok * out.nb + blk] = mm;
+                    out.qs[(size_t) tok * out.nb + blk] = make_uint4(q0, q1, q2, q3);
+                }
+                if (xs41) act41_emit(tok, nb, blk, e, qword, dd, mm, (uint4 *) xm, xs41);
+            }
+            continue;
+        }
         float amax = fabsf(v);
         for (int o2 = 16; o2 > 0; o2 >>= 1) { const float w = __shfl_xor(amax, o2); amax = w > amax ? w : amax; }
         const float dd = amax / 7.0f;
@@ -255,8 +276,11 @@ bool attention_prompt_supported(int n_embd, int n_head, int n_ctx) {
 }
 
 hipError_t launch_attention_prompt(const AttnLaunch & A, uint16_t * p_scratch, void * xm, float * xda,
-                                   hipStream_t s) {
-    if (!attention_prompt_supported(A.n_embd, A.n_head, A.n_ctx) || A.out_qtype != Q4_0) return hipErrorNotSupported;
+                                   hipStream_t s, void * xs41) {
+    if (!attention_prompt_supported(A.n_embd, A.n_head, A.n_ctx)) return hipErrorNotSupported;
+    // Q4_1 writes its MFMA operands (xm + xs41) or nothing but the ActQ; Q4_0 xm + xda
+    if (A.out_qtype == Q4_1 ? (xm != nullptr) != (xs41 != nullptr) : A.out_qtype != Q4_0 || xs41)
+        return hipErrorNotSupported;
     const float scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
     constexpr int T = 32;
     EventSplit ev;
@@ -269,7 +293,8 @@ hipError_t launch_attention_prompt(const AttnLaunch & A, uint16_t * p_scratch, v
     const size_t lds2 = (size_t) 64 * A.n_ctx * 2;
     ev.last();
     LVK_LAUNCH(k_attn_p_pv, dim3(A.n_head, (A.n_tokens + 31) / 32, HD / 32), dim3(256), lds2, s, A.vc, p_scratch,
-               A.sp, A.n_embd, A.n_ctx, A.out, (uint2 *) xm, xda, A.out_f32);
+               A.sp, A.n_embd, A.n_ctx, A.out, (uint2 *) xm, xda, A.out_f32, A.out_qtype == Q4_1 ? 1 : 0,
+               (uint4 *) xs41);
     return hipGetLastError();
 }
 

@@ -154,13 +154,13 @@ struct AttnLaunch {
     int kv32 = 0;             // f32 K, V and queries (f16_kv = false): launch_attention only
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
-// prompt batches (N > 1, Q4_0 output): scores+softmax per (head, 32 tokens) then
+// prompt batches (N > 1, Q4_0 / Q4_1 output): scores+softmax per (head, 32 tokens) then
 // P.V per (head, 32 tokens, 32 dims) with the Wo quantization fused
-// (attention_prompt.hip).  p_scratch: H*N*n_ctx f16; xm/xda (optional): also
-// write the Wo input as the MFMA fragment image (mm_mfma.hip).
+// (attention_prompt.hip).  p_scratch: H*N*n_ctx f16; optional: also write the Wo
+// input as the MFMA operands -- Q4_0 xm/xda (mm_mfma.hip), Q4_1 xm/xs41 (mm_mfma41.hip).
 bool attention_prompt_supported(int n_embd, int n_head, int n_ctx);
 hipError_t launch_attention_prompt(const AttnLaunch & A, uint16_t * p_scratch, void * xm, float * xda,
-                                   hipStream_t s);
+                                   hipStream_t s, void * xs41 = nullptr);
 // count into bad_d[0] / bad_d[1] the softmax arguments h <= 0 whose exp computed in
 // double / with the device expf differs from exp_tab[h]; 0 means that mode
 // reproduces the host table exactly

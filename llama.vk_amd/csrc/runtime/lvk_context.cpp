@@ -331,10 +331,11 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
             at.exp_computed = exp_computed;
             at.err = err_d;
             at.kv32 = kv32;
-            if (!q41 && !kv32 && attention_prompt_supported(E, H, n_ctx)) {
-                // writes the Wo input in both forms (ActQ and the MFMA fragment image)
+            if (!kv32 && attention_prompt_supported(E, H, n_ctx)) {
+                // writes the Wo input in both forms (ActQ and the MFMA operand images)
                 timed_launch(K_ATTN, 0, [&] {
-                    return launch_attention_prompt(at, (uint16_t *) scores, xh, xda, stream);
+                    return q41 ? launch_attention_prompt(at, (uint16_t *) scores, xh, nullptr, stream, xside)
+                               : launch_attention_prompt(at, (uint16_t *) scores, xh, xda, stream);
                 });
             } else {
                 timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
@@ -404,7 +405,7 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
                 return launch_attention_wo(at, ly.wo, x, attn_gran, (unsigned) il + 1, stream);
             });
         } else {
-            if (n > 1 && !kv32 && model.qtype == Q4_0 && attention_prompt_supported(E, H, n_ctx))
+            if (n > 1 && !kv32 && attention_prompt_supported(E, H, n_ctx))
                 timed_launch(K_ATTN, 0, [&] {
                     return launch_attention_prompt(at, (uint16_t *) scores, nullptr, nullptr, stream);
                 });

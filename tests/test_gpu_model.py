@@ -243,14 +243,17 @@ def test_mfma_prompt_7b_shaped_vs_oracle(lvk, oracle, model_dir, monkeypatch, a1
     om.close()
 
 
-def test_mfma_prompt_13b_q4_1_shaped_vs_oracle(lvk, oracle, model_dir):
+@pytest.mark.parametrize("n_ctx", [256, 2048])
+def test_mfma_prompt_13b_q4_1_shaped_vs_oracle(lvk, oracle, model_dir, n_ctx):
     """LLaMA-13B layer shapes in Q4_1 (K = 5120 / 13824, 40 heads), 2 layers: a 100-token
     prompt (ragged token tile) through the Q4_1 MFMA matmuls (mm_mfma41.hip), then decode on
-    the KV cache it wrote, bit-exact against the oracle"""
+    the KV cache it wrote, bit-exact against the oracle.  The Wo input comes from the prompt
+    attention's fused Q4_1 epilogue (n_ctx 256) or from the generic attention's ActQ via
+    launch_actq41_to_f16 (n_ctx 2048, past the prompt attention's LDS window)"""
     from oracle_lib import gen_model
     path = gen_model(os.path.join(model_dir, "w5120_l2_q41.bin"), n_embd=5120, n_head=40, n_layer=2, ftype=3, seed=11)
-    m = lvk.Llama(path, n_ctx=256)
-    om = oracle.model(path, 256)
+    m = lvk.Llama(path, n_ctx=n_ctx)
+    om = oracle.model(path, n_ctx)
     toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 100)], np.int32)
     m.set_profiling(True)
     m.reset_profile()

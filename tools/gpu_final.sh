@@ -10,5 +10,6 @@ tail -2 $O/gputests.log
 timeout -k 10 900 python3 -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 2; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt7 -o run --output-format csv -- python3 bench.py --steps 16 --warmup 4 --no-13b --no-65b --no-cpu-baseline --prompt-evals 1 > $O/kt7.log 2>&1 || exit 3
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt13 -o run --output-format csv -- python3 tools/decode_speed.py 13b 16 > $O/kt13.log 2>&1 || exit 4
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt13p -o run --output-format csv -- python3 tools/prompt_speed.py 512 13b > $O/kt13p.log 2>&1 || exit 5
 find $O -name '*kernel_stats.csv'
 echo final-ok
