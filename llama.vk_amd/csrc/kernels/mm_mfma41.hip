@@ -69,6 +69,55 @@ struct Blk {                 // one block's operands of one lane
     uint4 a[2], b[2], sa, sb;
 };
 
+// AVX2 horizontal order + offset, then the role's store (shared by both kernels)
+template <int EPI>
+__device__ __forceinline__ void epilogue41(const Mm41Params & P, const f32x16_t (&acc)[4], const f32x16_t & off,
+                                           int lane, int w, int m0, int n0) {
+    // AVX2 horizontal order (ggml.c:2250-2256) as in mm_mfma.hip, then + off * 32 (QK)
+    const int jj = (lane >> 4) & 1, h = lane >> 5;
+    float res[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float r0 = acc[0][i] + acc[2][i];
+        const float r2 = acc[1][i] + acc[3][i];
+        const float v = r0 + r2;
+        const float hs = v + __shfl_xor(v, 16);
+        res[i] = hs + off[i] * 32.0f;
+    }
+    const int n = n0 + (lane & 15);
+    if constexpr (EPI == EPI_SWIGLU_F32) {
+        float o[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[i] = __shfl_xor(res[i], 32);
+        if (jj == 0 && h == 0 && n < P.N) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float uu[4];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res[4 * q + p])]);  // ggml.c:2495
+                    uu[p] = sl * o[4 * q + p];                                            // llama.cpp:1096
+                }
+                const int row = m0 + 32 * w + 8 * q;
+                *(float4 *) (P.y + (size_t) n * P.ldy + row / 2) = make_float4(uu[0], uu[1], uu[2], uu[3]);
+            }
+        }
+    } else {
+        if (jj == 0 && n < P.N) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float4 * yp = (float4 *) (P.y + (size_t) n * P.ldy + m0 + 32 * w + 8 * q + 4 * h);
+                if constexpr (EPI == EPI_RESID) {
+                    const float4 r = *yp;
+                    *yp = make_float4(res[4 * q] + r.x, res[4 * q + 1] + r.y, res[4 * q + 2] + r.z, res[4 * q + 3] + r.w);
+                } else {
+                    *yp = make_float4(res[4 * q], res[4 * q + 1], res[4 * q + 2], res[4 * q + 3]);
+                }
+            }
+        }
+    }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(NT, 2) void k_mm_q41_mfma(Mm41Params P) {
     const int tid = threadIdx.x;
@@ -149,49 +198,119 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q41_mfma(Mm41Params P) {
         }
     }
 
-    // AVX2 horizontal order (ggml.c:2250-2256) as in mm_mfma.hip, then + off * 32 (QK)
-    const int jj = (lane >> 4) & 1, h = lane >> 5;
-    float res[16];
+    epilogue41<EPI>(P, acc, off, lane, w, m0, n0);
+}
+
+// ---------------------------------------------------------------------------
+// The same matmul with the operands streamed through a per-wave LDS ring by LDS-DMA
+// (global_load_lds_dwordx4, the decode_persistent.hip recipe).  hipcc's waitcnt pass
+// puts a vmcnt(0) at the register-ring loop's header (the refill issued last in a trip
+// is waited for at once); the DMAs are invisible to it, so the wave keeps RS blocks in
+// flight and waits with its own count.  Per wave RS slots of 6 x 1 KiB (a16 pair halves,
+// side, xm pair halves, xs: one 16-byte lane row each, read back with one ds_read_b128
+// per lane and operand); 72 KiB per workgroup, two workgroups per CU.
+// ---------------------------------------------------------------------------
+constexpr int RS = 3;                       // ring slots (blocks in flight) per wave
+constexpr int SLOT = 6 * 1024;
+constexpr int LDS41 = 4 * RS * SLOT;
+
+__device__ __forceinline__ unsigned lds_addr41(const void * p) {
+    return (unsigned) (uintptr_t) (const __attribute__((address_space(3))) uint8_t *) p;
+}
+// one 1 KiB LDS-DMA: lane l's 16 bytes at gsrc land at LDS byte lds_dst + 16 l
+__device__ __forceinline__ void dma1k(const void * gsrc, unsigned lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NT, 2) void k_mm_q41_dma(Mm41Params P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = tid >> 6;
+    const int nwg = gridDim.x;
+    const int bid = blockIdx.x;
+    const int full = nwg & ~7;
+    const int L = bid < full ? (bid & 7) * (full >> 3) + (bid >> 3) : bid;
+    const int tt = L % P.ntt;
+    const int m0 = (L / P.ntt) * TM;
+    const int n0 = tt * TN;
+    const int nb = P.nb;
+    const int rt = m0 / 32 + w;
+
+    const uint4 * ap = P.a16 + (size_t) rt * nb * 128 + lane;
+    const uint4 * sap = P.side + (size_t) rt * nb * 64 + lane;
+    const uint4 * bp = P.xm + (size_t) tt * nb * 128 + lane;
+    const uint4 * sbp = P.xs + (size_t) tt * nb * 64 + lane;
+    uint8_t * ring = smem + w * RS * SLOT;
+    const unsigned ring_l = __builtin_amdgcn_readfirstlane(lds_addr41(ring));
+    auto issue = [&](int blk, int slot) {
+        const unsigned d = ring_l + slot * SLOT;
+        dma1k(ap + (size_t) blk * 128, d);
+        dma1k(ap + (size_t) blk * 128 + 64, d + 1024);
+        dma1k(sap + (size_t) blk * 64, d + 2048);
+        dma1k(bp + (size_t) blk * 128, d + 3072);
+        dma1k(bp + (size_t) blk * 128 + 64, d + 4096);
+        dma1k(sbp + (size_t) blk * 64, d + 5120);
+    };
+
+    f32x16_t acc[4], off;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const float r0 = acc[0][i] + acc[2][i];
-        const float r2 = acc[1][i] + acc[3][i];
-        const float v = r0 + r2;
-        const float hs = v + __shfl_xor(v, 16);
-        res[i] = hs + off[i] * 32.0f;
-    }
-    const int n = n0 + (lane & 15);
-    if constexpr (EPI == EPI_SWIGLU_F32) {
-        float o[16];
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) o[i] = __shfl_xor(res[i], 32);
-        if (jj == 0 && h == 0 && n < P.N) {
+        for (int i = 0; i < 16; ++i) acc[c][i] = 0.0f;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float uu[4];
+    for (int i = 0; i < 16; ++i) off[i] = 0.0f;
+
 #pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res[4 * q + p])]);  // ggml.c:2495
-                    uu[p] = sl * o[4 * q + p];                                            // llama.cpp:1096
-                }
-                const int row = m0 + 32 * w + 8 * q;
-                *(float4 *) (P.y + (size_t) n * P.ldy + row / 2) = make_float4(uu[0], uu[1], uu[2], uu[3]);
+    for (int sl = 0; sl < RS; ++sl) issue(min(sl, nb - 1), sl);
+
+    int slot = 0;
+    for (int blk = 0; blk < nb; ++blk) {
+        // this block's 6 DMAs landed: at most the later RS - 1 blocks' are still in flight
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 * (RS - 1)) : "memory");
+        const uint4 * sp = (const uint4 *) (ring + slot * SLOT) + lane;   // ds_read (LDS pointer inferred)
+        Blk o;
+        o.a[0] = sp[0]; o.a[1] = sp[64]; o.sa = sp[128];
+        o.b[0] = sp[192]; o.b[1] = sp[256]; o.sb = sp[320];
+        // the slot is free once its reads returned: refill it RS blocks ahead
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(min(blk + RS, nb - 1), slot);
+        slot = slot + 1 == RS ? 0 : slot + 1;
+
+        const float sw = __builtin_bit_cast(float, o.sa.z);
+        const float sb1 = __builtin_bit_cast(float, o.sb.z);
+        const float sb2 = __builtin_bit_cast(float, o.sb.w);
+        const f32x32_t SM = __builtin_amdgcn_mfma_f32_32x32x1f32(sw, sb1, (f32x32_t){}, 0, 0, 0);
+        const f32x16_t SX = __builtin_amdgcn_mfma_f32_32x32x2f32(sw, sb2, (f32x16_t){}, 0, 0, 0);
+        const half4_t ax = __builtin_bit_cast(half4_t, make_uint2(o.sa.x, o.sa.y));
+        const uint32_t bfr[8] = {o.b[0].x, o.b[0].y, o.b[0].z, o.b[0].w, o.b[1].x, o.b[1].y, o.b[1].z, o.b[1].w};
+        const uint32_t afr[8] = {o.a[0].x, o.a[0].y, o.a[0].z, o.a[0].w, o.a[1].x, o.a[1].y, o.a[1].z, o.a[1].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const half4_t a = __builtin_bit_cast(half4_t, make_uint2(afr[2 * c], afr[2 * c + 1]));
+            const half4_t b = __builtin_bit_cast(half4_t, make_uint2(bfr[2 * c], bfr[2 * c + 1]));
+            const uint32_t yw = (c < 2) ? o.sb.x : o.sb.y;
+            const uint32_t ym = yw & ((c & 1) ? 0xFFFF0000u : 0x0000FFFFu);
+            const half4_t bs = __builtin_bit_cast(half4_t, (c < 2) ? make_uint2(ym, 0u) : make_uint2(0u, ym));
+            const f32x16_t Pc = __builtin_amdgcn_mfma_f32_32x32x8f16(a, b, (f32x16_t){}, 0, 0, 0);
+            const f32x16_t Sc = __builtin_amdgcn_mfma_f32_32x32x8f16(ax, bs, (f32x16_t){}, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                acc[c][i] = __builtin_fmaf(SM[i], Pc[i], acc[c][i]);      // ggml.c:2244
+                acc[c][i] = __builtin_fmaf(SX[i], Sc[i], acc[c][i]);      // ggml.c:2247
             }
         }
-    } else {
-        if (jj == 0 && n < P.N) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float4 * yp = (float4 *) (P.y + (size_t) n * P.ldy + m0 + 32 * w + 8 * q + 4 * h);
-                if constexpr (EPI == EPI_RESID) {
-                    const float4 r = *yp;
-                    *yp = make_float4(res[4 * q] + r.x, res[4 * q + 1] + r.y, res[4 * q + 2] + r.z, res[4 * q + 3] + r.w);
-                } else {
-                    *yp = make_float4(res[4 * q], res[4 * q + 1], res[4 * q + 2], res[4 * q + 3]);
-                }
-            }
-        }
+        for (int i = 0; i < 16; ++i) off[i] = off[i] + SM[16 + i];      // ggml.c:2226
+#pragma unroll
+        for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(acc[c]));
     }
+    // the trailing refills must land before the workgroup's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    epilogue41<EPI>(P, acc, off, lane, w, m0, n0);
 }
 
 // activation quantizer for the Q4_1 MFMA path: x[t] (optionally rms_norm * g) ->
@@ -337,12 +456,21 @@ hipError_t launch_mm_mfma41(const QMatrix & w, const void * xm, const void * xs,
     P.M = w.M; P.nb = w.K / 32; P.N = N; P.ntt = (N + TN - 1) / TN;
     P.y = y; P.ldy = ldy; P.silu_tab = silu_tab;
     const dim3 grid((w.M / TM) * P.ntt);
+    // LVK_MM41_DMA=0: the register-ring kernel instead of the LDS-DMA ring
+    const char * dma_env = getenv("LVK_MM41_DMA");
+    const bool dma = !dma_env || atoi(dma_env) != 0;
+#define LVK_MM41_GO(E)                                                                   \
+    do {                                                                                 \
+        if (dma) LVK_LAUNCH(k_mm_q41_dma<E>, grid, dim3(NT), LDS41, s, P);               \
+        else LVK_LAUNCH(k_mm_q41_mfma<E>, grid, dim3(NT), 0, s, P);                      \
+    } while (0)
     switch (epi) {
-        case EPI_STORE: LVK_LAUNCH(k_mm_q41_mfma<EPI_STORE>, grid, dim3(NT), 0, s, P); break;
-        case EPI_RESID: LVK_LAUNCH(k_mm_q41_mfma<EPI_RESID>, grid, dim3(NT), 0, s, P); break;
-        case EPI_SWIGLU_F32: LVK_LAUNCH(k_mm_q41_mfma<EPI_SWIGLU_F32>, grid, dim3(NT), 0, s, P); break;
+        case EPI_STORE: LVK_MM41_GO(EPI_STORE); break;
+        case EPI_RESID: LVK_MM41_GO(EPI_RESID); break;
+        case EPI_SWIGLU_F32: LVK_MM41_GO(EPI_SWIGLU_F32); break;
         default: return hipErrorInvalidValue;
     }
+#undef LVK_MM41_GO
     return hipGetLastError();
 }
 

@@ -216,9 +216,12 @@ def test_mul_mat_mfma_bit_exact(lvk, oracle, monkeypatch, m, k, n, norm, a16):
 # products on the matrix cores, ggml_vec_dot_q4_1's chains on the VALU -> bit-exact.
 # Shapes: LLaMA-13B rows (K 5120 / 13824), ragged token tiles, a 130-token batch; blocks
 # with d = 0 (all-zero and constant activations, constant weight blocks).
+@pytest.mark.parametrize("dma", ["1", "0"])
 @pytest.mark.parametrize("m,k,n,norm", [(128, 256, 2, False), (256, 5120, 40, True), (128, 13824, 17, False),
                                         (384, 1024, 130, True), (128, 4096, 16, False), (128, 5120, 3, True)])
-def test_mul_mat_mfma_q4_1_bit_exact(lvk, oracle, m, k, n, norm):
+def test_mul_mat_mfma_q4_1_bit_exact(lvk, oracle, monkeypatch, m, k, n, norm, dma):
+    """both operand streams: the LDS-DMA ring (default) and the register ring (LVK_MM41_DMA=0)"""
+    monkeypatch.setenv("LVK_MM41_DMA", dma)
     rng = np.random.default_rng(7 * m + k + 13 * n)
     w = (rng.standard_normal((m, k)) * 0.02).astype(np.float32)
     w[1, 32:64] = 0.01                                # a constant weight block (d = 0, m = 0.01)
