@@ -210,7 +210,14 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q41_mfma(Mm41Params P) {
 // side, xm pair halves, xs: one 16-byte lane row each, read back with one ds_read_b128
 // per lane and operand); 72 KiB per workgroup, two workgroups per CU.
 // ---------------------------------------------------------------------------
-constexpr int RS = 3;                       // ring slots (blocks in flight) per wave
+#ifndef LVK_MM41_RS
+#define LVK_MM41_RS 3
+#endif
+#ifndef LVK_MM41_OCC
+#define LVK_MM41_OCC 2
+#endif
+constexpr int RS = LVK_MM41_RS;             // ring slots (blocks in flight) per wave
+constexpr int OCC41 = LVK_MM41_OCC;         // workgroups per CU (LDS: OCC41 * LDS41 <= 160 KiB)
 constexpr int SLOT = 6 * 1024;
 constexpr int LDS41 = 4 * RS * SLOT;
 
@@ -225,7 +232,7 @@ __device__ __forceinline__ void dma1k(const void * gsrc, unsigned lds_dst) {
 }
 
 template <int EPI>
-__global__ __launch_bounds__(NT, 2) void k_mm_q41_dma(Mm41Params P) {
+__global__ __launch_bounds__(NT, OCC41) void k_mm_q41_dma(Mm41Params P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
