@@ -300,11 +300,24 @@ def decode_65b(args, rank, pg, n_ctx, ptoks):
         tok = int(np.argmax(m.eval([tok], 16 + i * 60)[-1]))
     prof = m.profile()
     m.set_profiling(False)
+    # 1-GPU 65B 512-token prompt (best of 2): the S = 1 reference point of the split's prefill
+    ptoks512 = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, n_ctx)], np.int32)
+    best = 1e30
+    for _ in range(2):
+        barrier(pg)
+        t0 = time.perf_counter()
+        m.eval(ptoks512, 0)
+        best = min(best, all_max(pg, time.perf_counter() - t0))
     m.close()
+    fmas = 80 * (4 * 8192 * 8192 + 3 * 8192 * 22016) / 4 * len(ptoks512)
+    prompt = {"value": len(ptoks512) / best, "unit": "tok/s", "n_tokens": len(ptoks512), "ms": best * 1e3,
+              "roofline": {"bound": "valu-fp32 (the reference's sequential fp32 FMA chains)",
+                           "achieved": 2 * fmas / best / 1e12, "peak": VALU_FP32_TFLOPS, "unit": "TFLOP/s",
+                           "frac": 2 * fmas / best / 1e12 / VALU_FP32_TFLOPS, "fp32_chain_fmas": fmas}}
     kernels = {k: {"avg_us": v["ms"] / v["launches"] * 1e3,
                    "gbs": (v["bytes"] / v["launches"]) / (v["ms"] / v["launches"] * 1e-3) / 1e9 if v["bytes"] else None}
                for k, v in prof.items() if v["launches"]}
-    return {"value": r, "unit": "tok/s", "steps": args.steps_65b, "ms_per_token": 1e3 / r,
+    return {"value": r, "unit": "tok/s", "steps": args.steps_65b, "ms_per_token": 1e3 / r, "prompt_eval": prompt,
             "workload": "LLaMA-65B Q4_0 (synthetic, seed 3; n_embd 8192, 64 heads, 80 layers, n_ff 22016) "
                         "single-stream greedy decode on 1 GPU, positions 16..%d, n_ctx %d"
                         % (16 + min(args.steps_65b, n_ctx - 16) - 1, n_ctx),

@@ -218,6 +218,9 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q41_mfma(Mm41Params P) {
 #endif
 constexpr int RS = LVK_MM41_RS;             // ring slots (blocks in flight) per wave
 constexpr int OCC41 = LVK_MM41_OCC;         // workgroups per CU (LDS: OCC41 * LDS41 <= 160 KiB)
+#ifndef LVK_MM41_PIPE
+#define LVK_MM41_PIPE 0
+#endif
 constexpr int SLOT = 6 * 1024;
 constexpr int LDS41 = 4 * RS * SLOT;
 
@@ -295,21 +298,44 @@ __global__ __launch_bounds__(NT, OCC41) void k_mm_q41_dma(Mm41Params P) {
         const half4_t ax = __builtin_bit_cast(half4_t, make_uint2(o.sa.x, o.sa.y));
         const uint32_t bfr[8] = {o.b[0].x, o.b[0].y, o.b[0].z, o.b[0].w, o.b[1].x, o.b[1].y, o.b[1].z, o.b[1].w};
         const uint32_t afr[8] = {o.a[0].x, o.a[0].y, o.a[0].z, o.a[0].w, o.a[1].x, o.a[1].y, o.a[1].z, o.a[1].w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        auto mfma_p = [&](int c) __attribute__((always_inline)) {
             const half4_t a = __builtin_bit_cast(half4_t, make_uint2(afr[2 * c], afr[2 * c + 1]));
             const half4_t b = __builtin_bit_cast(half4_t, make_uint2(bfr[2 * c], bfr[2 * c + 1]));
+            return __builtin_amdgcn_mfma_f32_32x32x8f16(a, b, (f32x16_t){}, 0, 0, 0);
+        };
+        auto mfma_s = [&](int c) __attribute__((always_inline)) {
             const uint32_t yw = (c < 2) ? o.sb.x : o.sb.y;
             const uint32_t ym = yw & ((c & 1) ? 0xFFFF0000u : 0x0000FFFFu);
             const half4_t bs = __builtin_bit_cast(half4_t, (c < 2) ? make_uint2(ym, 0u) : make_uint2(0u, ym));
-            const f32x16_t Pc = __builtin_amdgcn_mfma_f32_32x32x8f16(a, b, (f32x16_t){}, 0, 0, 0);
-            const f32x16_t Sc = __builtin_amdgcn_mfma_f32_32x32x8f16(ax, bs, (f32x16_t){}, 0, 0, 0);
+            return __builtin_amdgcn_mfma_f32_32x32x8f16(ax, bs, (f32x16_t){}, 0, 0, 0);
+        };
+#if LVK_MM41_PIPE
+        // software pipeline: chain pair c+1's MFMAs are issued before chain pair c's FMAs
+        f32x16_t Pn = mfma_p(0), Sn = mfma_s(0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const f32x16_t Pc = Pn, Sc = Sn;
+            if (c < 3) { Pn = mfma_p(c + 1); Sn = mfma_s(c + 1); }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                acc[c][i] = __builtin_fmaf(SM[i], Pc[i], acc[c][i]);      // ggml.c:2244
+                acc[c][i] = __builtin_fmaf(SX[i], Sc[i], acc[c][i]);      // ggml.c:2247
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#else
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const f32x16_t Pc = mfma_p(c);
+            const f32x16_t Sc = mfma_s(c);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 acc[c][i] = __builtin_fmaf(SM[i], Pc[i], acc[c][i]);      // ggml.c:2244
                 acc[c][i] = __builtin_fmaf(SX[i], Sc[i], acc[c][i]);      // ggml.c:2247
             }
         }
+#endif
 #pragma unroll
         for (int i = 0; i < 16; ++i) off[i] = off[i] + SM[16 + i];      // ggml.c:2226
 #pragma unroll
