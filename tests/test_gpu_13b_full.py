@@ -1,0 +1,71 @@
+"""Full-size LLaMA-13B Q4_1 parity (BASELINE.json configs[3], the second quant format): the
+real 40 x 5120 synthetic 13B Q4_1 model -- the same seeded file bench.py measures -- through
+the GPU library, compared with the REFERENCE build (oracle/_ref/libref.so, the AVX2 ggml.c
+path compiled from the reference sources) on the same tokens and the same batch chunking:
+
+  * a 16-token prompt batch (the Q4_1 MFMA prompt path, mm_mfma41.hip) then 4 greedy decode
+    steps (the CU-balanced Q4_1 decode kernels, matvec_cu41.hip);
+  * one 512-token prompt batch.
+
+The bar is bit-identical logits, as for the full 7B (tests/test_gpu_7b_full.py).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+MODEL = "/tmp/lvk_bench/llama-13b-q4_1.bin"    # bench.py's file (same generator, seed and shape)
+CFG = dict(n_embd=5120, n_head=40, n_layer=40, ftype=3, seed=2)
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def model13b(gpu_available):
+    from oracle_lib import gen_model
+    os.makedirs(os.path.dirname(MODEL), exist_ok=True)
+    if not os.path.exists(MODEL):
+        tmp = MODEL + ".tmp%d" % os.getpid()
+        gen_model(tmp, **CFG)
+        os.replace(tmp, MODEL)
+    return MODEL
+
+
+def _threads():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def test_13b_q4_1_full_prompt16_decode_vs_reference(model13b, ref):
+    import lvk
+    from oracle_lib import prompt_tokens
+    m = lvk.Llama(model13b, n_ctx=512)
+    rm = ref.model(model13b, 512)
+    toks = prompt_tokens(16)
+    a = m.eval(toks, 0)
+    b = rm.eval(toks, 0, n_threads=_threads())
+    assert np.array_equal(bits(a[-1]), bits(b[-1])), "16-token prompt logits differ"
+    n_past, tok = 16, int(np.argmax(b[-1]))
+    for _ in range(4):
+        a = m.eval([tok], n_past)
+        b = rm.eval([tok], n_past, n_threads=_threads())
+        assert np.array_equal(bits(a[-1]), bits(b[-1])), "decode logits differ at n_past %d" % n_past
+        n_past += 1
+        tok = int(np.argmax(b[-1]))
+    m.close()
+    rm.close()
+
+
+def test_13b_q4_1_full_prompt512_vs_reference(model13b, ref):
+    import lvk
+    from oracle_lib import prompt_tokens
+    m = lvk.Llama(model13b, n_ctx=512)
+    rm = ref.model(model13b, 512)
+    toks = prompt_tokens(512)
+    a = m.eval(toks, 0)
+    b = rm.eval(toks, 0, n_threads=_threads())
+    assert np.array_equal(bits(a[-1]), bits(b[-1])), "512-token prompt logits differ"
+    m.close()
+    rm.close()
