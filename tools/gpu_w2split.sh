@@ -1,10 +1,10 @@
-# W2 split-chain kernel (LVK_W2_SPLIT=1): 7B-shaped and full-7B parity with it on, 7B decode speed on/off
+# W2 split-chain kernel (LVK_W2_SPLIT=1) ring variants: parity with it on, 7B decode speed
 set -o pipefail
 mkdir -p gpurun_out
-LVK_W2_SPLIT=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_model.py tests/test_gpu_7b_full.py -k "7b_shaped_decode or 7b_full_prompt16" > gpurun_out/t_w2s.log 2>&1 || { tail -30 gpurun_out/t_w2s.log; exit 1; }
-tail -2 gpurun_out/t_w2s.log
-timeout -k 10 300 python -u tools/decode_speed.py 7b 256 > gpurun_out/w2s.log 2>&1 || { tail -20 gpurun_out/w2s.log; exit 2; }
-LVK_W2_SPLIT=1 timeout -k 10 300 python -u tools/decode_speed.py 7b 256 >> gpurun_out/w2s.log 2>&1 || { tail -20 gpurun_out/w2s.log; exit 3; }
-timeout -k 10 300 python -u tools/decode_speed.py 7b 256 >> gpurun_out/w2s.log 2>&1 || { tail -20 gpurun_out/w2s.log; exit 4; }
-LVK_W2_SPLIT=1 timeout -k 10 300 python -u tools/decode_speed.py 7b 256 >> gpurun_out/w2s.log 2>&1 || { tail -20 gpurun_out/w2s.log; exit 5; }
-grep model gpurun_out/w2s.log
+LVK_W2_SPLIT=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_model.py -k "w2_split" > gpurun_out/t_w2s.log 2>&1 || { tail -30 gpurun_out/t_w2s.log; exit 1; }
+for v in w2r8 w2r12; do LVK_LIB=$PWD/llama.vk_amd/lib/$v/libllama_vk_amd.so LVK_W2_SPLIT=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_model.py -k "w2_split" >> gpurun_out/t_w2s.log 2>&1 || { tail -30 gpurun_out/t_w2s.log; exit 1; }; done
+grep passed gpurun_out/t_w2s.log
+timeout -k 10 300 python -u tools/decode_speed.py 7b 256 > gpurun_out/w2s.log 2>&1 || exit 2
+LVK_W2_SPLIT=1 timeout -k 10 300 python -u tools/decode_speed.py 7b 256 >> gpurun_out/w2s.log 2>&1 || exit 3
+for v in w2r8 w2r12; do LVK_LIB=$PWD/llama.vk_amd/lib/$v/libllama_vk_amd.so LVK_W2_SPLIT=1 timeout -k 10 300 python -u tools/decode_speed.py 7b 256 >> gpurun_out/w2s.log 2>&1 || exit 4; done
+grep model gpurun_out/w2s.log | cut -c1-230
