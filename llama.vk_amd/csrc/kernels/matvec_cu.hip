@@ -473,9 +473,9 @@ __global__ __launch_bounds__(256) void k_mv_w2split(CuParams P) {
     };
     constexpr int NCW = C0 > NC1 ? C0 : NC1;
 #ifndef LVK_W2S_RING
-#define LVK_W2S_RING 8
+#define LVK_W2S_RING 4
 #endif
-    constexpr int RING = LVK_W2S_RING;          // sub-chunks in flight per wave (all: 13.5 us, 12: 11.7, 8: 11.2)
+    constexpr int RING = LVK_W2S_RING;          // sub-chunks in flight per wave (all: 13.5 us, 12: 11.7, 8: 11.2, 4: 10.5, 2: 11.1)
     uint4 W[RING];
     float4 S[NCW];
     const int sbase = part == 0 ? 0 : H;
