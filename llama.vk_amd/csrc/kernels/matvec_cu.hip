@@ -421,11 +421,14 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
 // doing half of the dot/convert work and all weight loads of a wave issued at once
 // (static counts: K is a template constant, the loops are fully unrolled).
 // ---------------------------------------------------------------------------
+#ifndef LVK_W2S_H
+#define LVK_W2S_H 0          // sub-chunks of part 0 (0: half)
+#endif
 template <int KT>
 __global__ __launch_bounds__(256) void k_mv_w2split(CuParams P) {
     constexpr int NW = 4, RG = 2;               // 2 row groups x 2 parts per workgroup
     constexpr int nb = KT / 32, nsub = nb / 8, NC = (nb + 31) / 32;
-    constexpr int H = (nsub + 1) / 2;           // sub-chunks of part 0
+    constexpr int H = LVK_W2S_H > 0 ? LVK_W2S_H : (nsub + 1) / 2;   // sub-chunks of part 0
     constexpr int NS1 = nsub - H;               // sub-chunks of part 1
     constexpr int NB1 = NS1 * 8;                // blocks of part 1
     constexpr int C0 = (H * 4 + 15) / 16;       // chunks part 0 touches (sub-chunk s -> chunk s / 4)
@@ -689,7 +692,8 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 8192>(P, s);
     } else if (K == 11008) {
         if (epi == EPI_RESID && pro == PRO_ACTF && w2_split_env() && (P.G + cu_count() - 1) / cu_count() <= 2) {
-            constexpr int nb = 11008 / 32, nsub = nb / 8, NB1 = (nsub - (nsub + 1) / 2) * 8, NC = (nb + 31) / 32;
+            constexpr int nb = 11008 / 32, nsub = nb / 8, NC = (nb + 31) / 32;
+            constexpr int NB1 = (nsub - (LVK_W2S_H > 0 ? LVK_W2S_H : (nsub + 1) / 2)) * 8;
             const size_t lds = (size_t) nb * 32 + NC * 128 + 4 * 2 * SPL * 4 + 2 * 64 * (NB1 + 4) * 4 + 2 * NB1 * 8 * 4;
             LVK_LAUNCH(k_mv_w2split<11008>, dim3(std::min(cu_count(), P.G)), dim3(256), lds, s, P);
             return hipGetLastError();
