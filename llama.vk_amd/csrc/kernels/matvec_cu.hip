@@ -422,7 +422,7 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
 // (static counts: K is a template constant, the loops are fully unrolled).
 // ---------------------------------------------------------------------------
 #ifndef LVK_W2S_H
-#define LVK_W2S_H 0          // sub-chunks of part 0 (0: half)
+#define LVK_W2S_H 26         // sub-chunks of part 0 of 43 (22: 10.5 us, 26: 9.9, 30: 10.0; 0: half)
 #endif
 template <int KT>
 __global__ __launch_bounds__(256) void k_mv_w2split(CuParams P) {
