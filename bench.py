@@ -59,41 +59,109 @@ class _StdoutToStderr:
         os.close(self.saved)
 
 
-def dist_setup():
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    pg = None
-    if ws > 1:
-        import torch.distributed as dist
-        with _StdoutToStderr():
-            dist.init_process_group("gloo")
-        pg = dist
-    return ws, rank, local, pg
+class LocalCoord:
+    """N = 1: no peers"""
+    rank, ws, local = 0, 1, 0
 
+    def barrier(self):
+        pass
 
-def barrier(pg):
-    if pg is not None:
-        pg.barrier()
-
-
-def all_max(pg, v):
-    if pg is None:
+    def max(self, v):
         return v
+
+    def bcast(self, obj):
+        return obj
+
+
+class PipeCoord:
+    """N > 1, in the worker process: the barrier, max over ranks and broadcast from rank 0 are
+    asked of the parent (which holds the gloo group) over a pipe.  The worker imports lvk and
+    never torch; the parent imports torch and never lvk: one HIP runtime per process
+    (profiles/r03_runtime_mix.md)."""
+
+    def __init__(self, rfd, wfd):
+        self.r = os.fdopen(rfd, "r")
+        self.w = os.fdopen(wfd, "w")
+        self.ws = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    def _ask(self, op, v=None):
+        self.w.write(json.dumps({"op": op, "v": v}) + "\n")
+        self.w.flush()
+        line = self.r.readline()
+        if not line:
+            raise SystemExit("bench worker: parent closed the coordination pipe")
+        return json.loads(line)["v"]
+
+    def barrier(self):
+        self._ask("barrier")
+
+    def max(self, v):
+        return float(self._ask("max", v))
+
+    def bcast(self, obj):
+        return self._ask("bcast", obj)
+
+    def result(self, obj):
+        self._ask("result", obj)
+
+
+def serve_worker(argv):
+    """N > 1 parent (one per rank under torchrun): joins the gloo group, runs the GPU work in a
+    worker child (bench.py --worker) and answers its barrier / max / broadcast requests; rank 0
+    prints the JSON line the worker hands back.  Returns the worker's exit code."""
+    import datetime
+    import torch.distributed as dist
+    ws = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ["RANK"])
+    with _StdoutToStderr():
+        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=20))
+    p2c_r, p2c_w = os.pipe()
+    c2p_r, c2p_w = os.pipe()
+    env = dict(os.environ, LVK_BENCH_FDS="%d,%d" % (p2c_r, c2p_w))
+    child = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--worker"] + argv,
+                             pass_fds=(p2c_r, c2p_w), env=env, stdout=sys.stderr)
+    os.close(p2c_r)
+    os.close(c2p_w)
+    rd, wr = os.fdopen(c2p_r, "r"), os.fdopen(p2c_w, "w")
+    result = None
     import torch
-    t = torch.tensor([v], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
+    while True:
+        line = rd.readline()
+        if not line:
+            break
+        msg = json.loads(line)
+        op, v = msg["op"], msg["v"]
+        if op == "barrier":
+            dist.barrier()
+        elif op == "max":
+            t = torch.tensor([float(v)], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            v = float(t.item())
+        elif op == "bcast":
+            box = [v]
+            dist.broadcast_object_list(box, src=0)
+            v = box[0]
+        elif op == "result":
+            result = v
+        wr.write(json.dumps({"v": v}) + "\n")
+        wr.flush()
+    rc = child.wait()
+    if rank == 0 and result is not None:
+        print(json.dumps(result), flush=True)
+    dist.destroy_process_group()
+    return rc if result is not None or rank != 0 else (rc or 1)
 
 
-def ensure_model(path, rank, pg, cfg):
-    if rank == 0 and not os.path.exists(path):
+def ensure_model(path, coord, cfg):
+    if coord.rank == 0 and not os.path.exists(path):
         os.makedirs(os.path.dirname(path), exist_ok=True)
         import lvk
         tmp = path + ".tmp"
         lvk.gen_model(tmp, vocab=os.path.join(ROOT, "tests", "golden", "vocab32000.bin"), **cfg)
         os.replace(tmp, path)
-    barrier(pg)
+    coord.barrier()
 
 
 def cpu_info():
@@ -121,53 +189,65 @@ def cpu_info():
     return info
 
 
-def cpu_baseline(path, budget_s=20.0, label="7B Q4_0", prompt=True, seg_steps=16):
+def cpu_baseline(path, budget_s=20.0, label="7B Q4_0", prompt=True, seg_steps=16, n_seg=3):
     """The reference AVX2 ggml.c build (oracle/_ref/libref.so) on the same file and tokens:
-    decode tok/s best of 3 segments and (prompt=True) the 512-token prompt batch,
-    llama.cpp:1186-1195's n_eval / t_eval and n_p_eval / t_p_eval."""
+    decode tok/s (best of up to n_seg segments) at -t = the physical cores of this process's
+    CPU set (BASELINE.md section 4) and at the box's per-GPU share (OMP_NUM_THREADS, 16);
+    value = the faster of the two, and (prompt=True) the 512-token prompt batch at that
+    thread count -- llama.cpp:1186-1195's n_eval / t_eval and n_p_eval / t_p_eval."""
     from oracle_lib import REF_SO, Ref
     if not os.path.exists(REF_SO):
         return None
     import numpy as np
     info = cpu_info()
-    # the reference is run at -t = physical cores, capped by this job's CPU share: the GPU
-    # box runs one job per GPU with OMP_NUM_THREADS (16) threads of its many cores
     share = int(os.environ.get("OMP_NUM_THREADS") or 0) or 16
-    threads = max(1, min(info.get("physical_cores") or info["affinity"], share))
+    phys = info.get("physical_cores") or info["affinity"]
+    tried = []
+    for t in sorted({phys, min(share, phys)}, reverse=True):
+        tried.append(max(1, t))
     ref = Ref()
+    t_load = time.perf_counter()
     m = ref.model(path, 512)
+    t_load = time.perf_counter() - t_load
     toks = np.array(prompt_tokens(16), np.int32)
-    lg = m.eval(toks, 0, n_threads=threads)
-    tok, n_past = int(np.argmax(lg[-1])), 16
-    segs, t_used = [], 0.0
-    for _ in range(3):                                       # best of 3 decode segments
-        t0 = time.perf_counter()
-        for _ in range(seg_steps):
-            lg = m.eval(np.array([tok], np.int32), n_past, n_threads=threads)
-            tok = int(np.argmax(lg[-1]))
-            n_past += 1
-        dt = time.perf_counter() - t0
-        segs.append(seg_steps / dt)
-        t_used += dt
-        if t_used > budget_s / 2:
-            break
+    rates, t_used, n_past = {}, 0.0, 16
+    tok = 0
+    for threads in tried:
+        lg = m.eval(toks, 0, n_threads=threads)
+        tok, n_past = int(np.argmax(lg[-1])), 16
+        segs = []
+        for _ in range(n_seg):
+            t0 = time.perf_counter()
+            for _ in range(seg_steps):
+                lg = m.eval(np.array([tok], np.int32), n_past, n_threads=threads)
+                tok = int(np.argmax(lg[-1]))
+                n_past += 1
+            dt = time.perf_counter() - t0
+            segs.append(seg_steps / dt)
+            t_used += dt
+            if t_used > budget_s / 2:
+                break
+        rates[threads] = segs
+    best_t = max(rates, key=lambda t: max(rates[t]))
     p512 = np.array(prompt_tokens(512), np.int32)
     pr = []
     for _ in range(3 if prompt else 0):                      # 512-token prompt batch, best of up to 3
         t0 = time.perf_counter()
-        m.eval(p512, 0, n_threads=threads)
+        m.eval(p512, 0, n_threads=best_t)
         pr.append(512 / (time.perf_counter() - t0))
         t_used += 512 / pr[-1]
         if t_used > budget_s:
             break
     m.close()
-    out = {"value": max(segs), "unit": "tok/s", "cores": threads, "kind": "reference",
+    out = {"value": max(rates[best_t]), "unit": "tok/s", "cores": best_t, "kind": "reference",
            "sample": "reference ggml.c AVX2 build (oracle/_ref, compiled from the reference sources), the same "
-                     "synthetic %s file and tokens, n_ctx 512, f16 KV, -t %d: 16-token prompt, then best of "
-                     "%d segments of %d greedy decode steps (positions 16..%d)%s"
-                     % (label, threads, len(segs), seg_steps, n_past - 1,
-                        "; prompt = one 512-token batch, best of %d" % len(pr) if prompt else ""),
-           "decode_segments_tok_s": segs, "host": info}
+                     "synthetic %s file and tokens, n_ctx 512, f16 KV: 16-token prompt, then segments of %d "
+                     "greedy decode steps at -t %s (physical cores of the CPU set, and the per-GPU share); "
+                     "value = the faster thread count (-t %d)%s"
+                     % (label, seg_steps, " and ".join(str(t) for t in tried), best_t,
+                        "; prompt = one 512-token batch at -t %d, best of %d" % (best_t, len(pr)) if prompt else ""),
+           "decode_tok_s_by_threads": {str(t): max(v) for t, v in rates.items()},
+           "decode_segments_tok_s": rates[best_t], "load_s": t_load, "host": info}
     if prompt:
         out["prompt_tok_s"] = max(pr)
         out["prompt_runs_tok_s"] = pr
@@ -222,17 +302,17 @@ def split_child(args):
                       "prefill_s": pre[args.split_micro], "prefill_nomicro_s": pre[0]}), flush=True)
 
 
-def layer_split(args, rank, ws, local, pg):
+def layer_split(args, coord):
     """N > 1: LLaMA-65B Q4_0 (BASELINE configs[4]) split by layers over the ws ranks, one
     stage per GPU, residual stream over RCCL send/recv (the C++ stage link).  Each rank runs
     its stage in a child process under a time limit, so a transport failure costs this line,
     not the bench."""
     path = args.split_model or os.path.join(os.path.dirname(args.model), "llama-65b-q4_0.bin")
-    ensure_model(path, rank, pg, CFG_65B)
+    rank, ws, local = coord.rank, coord.ws, coord.local
+    ensure_model(path, coord, CFG_65B)
     import lvk
-    uid = [lvk.rccl_unique_id().hex() if rank == 0 else None]
-    if pg is not None:
-        pg.broadcast_object_list(uid, src=0)
+    # the communicator id is made here, in a process without torch (PipeCoord)
+    uid = [coord.bcast(lvk.rccl_unique_id().hex() if rank == 0 else None)]
     cmd = [sys.executable, os.path.abspath(__file__), "--split-child", "--split-stages", str(ws),
            "--split-stage", str(rank), "--split-device", str(local % lvk.device_count()), "--split-uid", uid[0],
            "--split-model", path, "--steps-split", str(args.steps_split), "--warmup", "4",
@@ -248,16 +328,12 @@ def layer_split(args, rank, ws, local, pg):
         err = "rank %d stage timed out after %d s" % (rank, SPLIT_TIMEOUT_S)
     except Exception as e:                       # noqa: BLE001 -- reported in the line
         err = "rank %d: %r" % (rank, e)
-    ok = all_max(pg, 0.0 if res is not None else 1.0) == 0.0
+    ok = coord.max(0.0 if res is not None else 1.0) == 0.0
     if not ok:
-        errs = [err]
-        if pg is not None:
-            errs = [None] * ws
-            pg.all_gather_object(errs, err)
-        return {"error": [e for e in errs if e]}
-    dec = all_max(pg, res["decode_s"])
-    pre = all_max(pg, res["prefill_s"])
-    pre0 = all_max(pg, res["prefill_nomicro_s"])
+        return {"error": err or "another rank's stage failed"}
+    dec = coord.max(res["decode_s"])
+    pre = coord.max(res["prefill_s"])
+    pre0 = coord.max(res["prefill_nomicro_s"])
     L = CFG_65B["n_layer"]
     r = args.steps_split / dec
     return {"value": r, "unit": "tok/s", "stages": ws, "steps": args.steps_split, "ms_per_token": 1e3 / r,
@@ -271,7 +347,7 @@ def layer_split(args, rank, ws, local, pg):
             "transport": "RCCL (ncclCommInitRank over the %d ranks)" % ws}
 
 
-def decode_65b(args, rank, pg, n_ctx, ptoks):
+def decode_65b(args, coord, n_ctx, ptoks):
     """LLaMA-65B Q4_0 single-stream decode on ONE GPU (BASELINE configs[4] at S = 1: the
     40.6 GB of weights fit in 288 GB of HBM): tok/s, fraction of the model-bytes roofline
     (197 tok/s at 8 TB/s) and a per-kernel-class profile"""
@@ -279,7 +355,7 @@ def decode_65b(args, rank, pg, n_ctx, ptoks):
     import lvk
     path = os.path.join(os.path.dirname(args.model), "llama-65b-q4_0.bin")
     t0 = time.time()
-    ensure_model(path, rank, pg, CFG_65B)
+    ensure_model(path, coord, CFG_65B)
     gen_s = time.time() - t0
     t0 = time.time()
     m = lvk.Llama(path, n_ctx=n_ctx)
@@ -288,11 +364,11 @@ def decode_65b(args, rank, pg, n_ctx, ptoks):
     tok = int(np.argmax(lg[-1]))
     for i in range(4):
         tok = int(np.argmax(m.eval([tok], 16 + i)[-1]))
-    barrier(pg)
+    coord.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps_65b):
         tok = int(np.argmax(m.eval([tok], 16 + (i % (n_ctx - 16)))[-1]))
-    dt = all_max(pg, time.perf_counter() - t0)
+    dt = coord.max(time.perf_counter() - t0)
     r = args.steps_65b / dt
     m.set_profiling(True)
     m.reset_profile()
@@ -304,11 +380,15 @@ def decode_65b(args, rank, pg, n_ctx, ptoks):
     ptoks512 = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, n_ctx)], np.int32)
     best = 1e30
     for _ in range(2):
-        barrier(pg)
+        coord.barrier()
         t0 = time.perf_counter()
         m.eval(ptoks512, 0)
-        best = min(best, all_max(pg, time.perf_counter() - t0))
+        best = min(best, coord.max(time.perf_counter() - t0))
     m.close()
+    cpu65 = None
+    if coord.rank == 0 and coord.ws == 1 and not args.no_cpu_baseline:
+        # the reference on the same 40.6 GB file: a few decode steps
+        cpu65 = cpu_baseline(path, args.cpu_budget, label="65B Q4_0", prompt=False, seg_steps=2, n_seg=2)
     fmas = 80 * (4 * 8192 * 8192 + 3 * 8192 * 22016) / 4 * len(ptoks512)
     prompt = {"value": len(ptoks512) / best, "unit": "tok/s", "n_tokens": len(ptoks512), "ms": best * 1e3,
               "roofline": {"bound": "valu-fp32 (the reference's sequential fp32 FMA chains)",
@@ -324,7 +404,8 @@ def decode_65b(args, rank, pg, n_ctx, ptoks):
             "model_bytes_per_token": MODEL_BYTES_65B,
             "frac_hbm_roofline": r * MODEL_BYTES_65B / 1e9 / HBM_PEAK_GBS,
             "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_65B,
-            "kernels": kernels, "gen_s": gen_s, "load_s": load_s}
+            "kernels": kernels, "gen_s": gen_s, "load_s": load_s, "cpu_baseline": cpu65,
+            "vs_cpu_baseline": (r / cpu65["value"]) if cpu65 else None}
 
 
 def main():
@@ -348,6 +429,8 @@ def main():
     ap.add_argument("--split-micro", type=int, default=64, help="prompt micro-batch of the layer split (tokens)")
     ap.add_argument("--split-rehearse", action="store_true",
                     help="run the layer-split leg at N = 1 too (one stage: the RCCL link on one rank)")
+    ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--coord-selftest", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--split-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--split-stages", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--split-stage", type=int, default=0, help=argparse.SUPPRESS)
@@ -359,8 +442,28 @@ def main():
     if args.split_child:
         split_child(args)
         return
+    if args.worker:
+        rfd, wfd = (int(x) for x in os.environ["LVK_BENCH_FDS"].split(","))
+        coord = PipeCoord(rfd, wfd)
+        coord.result(run(args, coord))
+        return
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        sys.exit(serve_worker(sys.argv[1:]))
+    out = run(args, LocalCoord())
+    print(json.dumps(out))
 
-    ws, rank, local, pg = dist_setup()
+
+def run(args, coord):
+    """every leg of the bench on this rank's GPU; returns rank 0's JSON object (None elsewhere)"""
+    ws, rank, local = coord.ws, coord.rank, coord.local
+    if args.coord_selftest:
+        # the N > 1 plumbing without a GPU (tests/test_bench_coord.py): no lvk, no torch here
+        coord.barrier()
+        mx = coord.max(float(rank + 1))
+        b = coord.bcast({"uid": "ab" * 64} if rank == 0 else None)
+        coord.barrier()
+        return {"ws": ws, "rank": rank, "max": mx, "bcast": b, "torch_in_worker": "torch" in sys.modules} \
+            if rank == 0 else None
     n_gpus = args.gpus if args.gpus else ws
     import numpy as np
     import lvk
@@ -369,7 +472,7 @@ def main():
     if ws > 1:
         lvk.set_device(local % lvk.device_count())
     cfg = dict(n_embd=4096, n_head=32, n_layer=32, ftype=2, seed=1)
-    ensure_model(args.model, rank, pg, cfg)
+    ensure_model(args.model, coord, cfg)
 
     t0 = time.time()
     m = lvk.Llama(args.model, n_ctx=512)
@@ -387,14 +490,14 @@ def main():
     # timed region: K greedy decode steps
     lg = m.eval(ptoks, 0)
     tok = int(np.argmax(lg[-1]))
-    barrier(pg)
+    coord.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
         lg = m.eval([tok], 16 + (i % (n_ctx - 16)))
         tok = int(np.argmax(lg[-1]))
     t1 = time.perf_counter()
-    barrier(pg)
-    elapsed = all_max(pg, t1 - t0)
+    coord.barrier()
+    elapsed = coord.max(t1 - t0)
     value = n_gpus * args.steps / elapsed
     last = 16 + min(args.steps, n_ctx - 16) - 1
     positions = "16..%d" % last + ("" if args.steps <= n_ctx - 16 else " (wrapping to 16 after 511)")
@@ -406,13 +509,13 @@ def main():
         m.eval(ptoks, 0)
         tok = int(np.argmax(m.logits()[-1]))
         tok_first = tok
-        barrier(pg)
+        coord.barrier()
         t0 = time.perf_counter()
         for i in range(args.steps):
             tok = m.eval_greedy(tok, 16 + (i % (n_ctx - 16)))
         t1 = time.perf_counter()
-        barrier(pg)
-        el_g = all_max(pg, t1 - t0)
+        coord.barrier()
+        el_g = coord.max(t1 - t0)
         greedy = {"value": n_gpus * args.steps / el_g, "unit": "tok/s", "ms_per_step": el_g / args.steps * 1e3,
                   "path": "lvk_eval_greedy: decode graph ending in the device argmax, 4-byte D2H",
                   "first_token": tok_first}
@@ -452,7 +555,7 @@ def main():
         t0 = time.perf_counter()
         m.eval(p512, 0)
         best = min(best, time.perf_counter() - t0)
-    best = all_max(pg, best)
+    best = coord.max(best)
     # the bit-faithful floor is the reference's fp32 chains -- one fmaf per
     # 4-element integer partial -- at the VALU FP32 peak; the INT8 line prices the same
     # matmul MACs on the dense matrix-core peak (what a non-faithful GEMM could reach)
@@ -510,19 +613,19 @@ def main():
     q41 = None
     if not args.no_13b:
         path13 = os.path.join(os.path.dirname(args.model), "llama-13b-q4_1.bin")
-        ensure_model(path13, rank, pg, dict(n_embd=5120, n_head=40, n_layer=40, ftype=3, seed=2))
+        ensure_model(path13, coord, dict(n_embd=5120, n_head=40, n_layer=40, ftype=3, seed=2))
         m13 = lvk.Llama(path13, n_ctx=n_ctx)
         lg = m13.eval(ptoks, 0)
         tok = int(np.argmax(lg[-1]))
         for i in range(4):
             lg = m13.eval([tok], 16 + i)
             tok = int(np.argmax(lg[-1]))
-        barrier(pg)
+        coord.barrier()
         t0 = time.perf_counter()
         for i in range(args.steps_13b):
             lg = m13.eval([tok], 16 + (i % (n_ctx - 16)))
             tok = int(np.argmax(lg[-1]))
-        t13 = all_max(pg, time.perf_counter() - t0)
+        t13 = coord.max(time.perf_counter() - t0)
         # per-kernel-class HIP-event pass (the Q4_1 decode kernels, matvec_cu41.hip)
         m13.set_profiling(True)
         m13.reset_profile()
@@ -535,10 +638,10 @@ def main():
         ptoks13 = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, n_ctx)], np.int32)
         best13 = 1e30
         for _ in range(3):
-            barrier(pg)
+            coord.barrier()
             t0 = time.perf_counter()
             m13.eval(ptoks13, 0)
-            best13 = min(best13, all_max(pg, time.perf_counter() - t0))
+            best13 = min(best13, coord.max(time.perf_counter() - t0))
         m13.close()
         E13, F13 = 5120, 13824
         fmas13 = 2.0 * 40 * (4 * E13 * E13 + 3 * E13 * F13) / 4 * len(ptoks13)   # 16 chain FMAs per 32 weights
@@ -567,41 +670,44 @@ def main():
     # the residual stream between stages)
     split = None
     if (ws > 1 or args.split_rehearse) and not args.no_split:
-        split = layer_split(args, rank, ws, local, pg)
+        split = layer_split(args, coord)
     d65 = None
     if ws == 1 and not args.no_65b:
-        d65 = decode_65b(args, rank, pg, n_ctx, ptoks)
+        d65 = decode_65b(args, coord, n_ctx, ptoks)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.model, args.cpu_budget)
 
-    if rank == 0:
-        out = {
-            "metric": "decode tok/s + prompt-eval tok/s, LLaMA-7B Q4_0; % HBM roofline",
-            "value": value, "unit": "tok/s", "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": value / REF_PUBLISHED_TOKS,
-            "dtype": "i4xi4->f32 (Q4_0 blocks, exact int dots, fp32 FMA chains)",
-            "data": "synthetic (seeded ggjt 7B Q4_0, lvk-gen-model seed 1)",
-            "config": {"workload": "LLaMA-7B Q4_0 single-stream decode: 16-token prompt then %d greedy decode "
-                                   "steps at positions %s, n_ctx 512, f16 KV" % (args.steps, positions),
-                       "n_ctx": n_ctx,
-                       "parallelism": "replicas" if n_gpus > 1 else "single-gpu"},
-            "roofline": roofline,
-            "step_roofline": {"model_bytes_per_token": MODEL_BYTES_7B, "achieved_gbs": step_gbs,
-                              "frac": step_gbs / HBM_PEAK_GBS, "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_7B},
-            "prompt_eval": prompt,
-            "decode_greedy_device": greedy,
-            "decode_13b_q4_1": q41,
-            "decode_65b_q4_0": d65,
-            "layer_split": split,
-            "kernels": kernels,
-            "cpu_baseline": cpu,
-            "load_s": load_s,
-        }
-        print(json.dumps(out))
-    if pg is not None:
-        pg.destroy_process_group()
+    if rank != 0:
+        return None
+    out = {
+        "metric": "decode tok/s + prompt-eval tok/s, LLaMA-7B Q4_0; % HBM roofline",
+        "value": value, "unit": "tok/s", "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": value / REF_PUBLISHED_TOKS,
+        "vs_baseline_note": "vs_baseline divides by the README's published 7B Q4_0 CPU figure (16.3 tok/s, Apple "
+                            "Silicon, BASELINE.md section 1); vs_cpu_baseline divides by the reference build timed "
+                            "on this box's host cores in this run (cpu_baseline)",
+        "vs_cpu_baseline": (value / n_gpus / cpu["value"]) if cpu else None,
+        "dtype": "i4xi4->f32 (Q4_0 blocks, exact int dots, fp32 FMA chains)",
+        "data": "synthetic (seeded ggjt 7B Q4_0, lvk-gen-model seed 1)",
+        "config": {"workload": "LLaMA-7B Q4_0 single-stream decode: 16-token prompt then %d greedy decode "
+                               "steps at positions %s, n_ctx 512, f16 KV" % (args.steps, positions),
+                   "n_ctx": n_ctx,
+                   "parallelism": "replicas" if n_gpus > 1 else "single-gpu"},
+        "roofline": roofline,
+        "step_roofline": {"model_bytes_per_token": MODEL_BYTES_7B, "achieved_gbs": step_gbs,
+                          "frac": step_gbs / HBM_PEAK_GBS, "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_7B},
+        "prompt_eval": prompt,
+        "decode_greedy_device": greedy,
+        "decode_13b_q4_1": q41,
+        "decode_65b_q4_0": d65,
+        "layer_split": split,
+        "kernels": kernels,
+        "cpu_baseline": cpu,
+        "load_s": load_s,
+    }
+    return out
 
 
 if __name__ == "__main__":

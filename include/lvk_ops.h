@@ -175,9 +175,18 @@ LVK_API int lvk_stage_layers(struct llama_context * ctx, int * layer_begin, int 
  * stage's layers, ncclSend to stage+1, all on the context's stream, prompts cut into
  * micro-batches of `micro` tokens (0: none).  greedy != 0 (one token): the last stage's
  * device argmax is sent to stage 0; both return it.  Otherwise 0 (the last stage leaves
- * logits for llama_get_logits).  -1 on error. */
+ * logits for llama_get_logits).  -1 on error.  Every argument is checked before the first
+ * transfer; a step that fails on any rank aborts the link (ncclCommAbort / the shm ring's
+ * abort word), so the neighbours' steps fail too instead of waiting, and every wait is
+ * bounded by LVK_STAGE_TIMEOUT_S seconds (default 300).  An aborted link must be
+ * reconnected.  The replaced code is the single-process llama_eval_internal
+ * (reference llama.cpp:927-1197). */
 LVK_API int lvk_rccl_unique_id(void * id, size_t n);
 LVK_API int lvk_stage_connect(struct llama_context * ctx, const void * id, int n_stages, int stage);
+/* The same link through a host shared-memory ring (POSIX shm object `name`, opened by every
+ * stage): any stage placement, several stages on one GPU included, no RCCL.  The call
+ * returns once all n_stages stages have opened the ring. */
+LVK_API int lvk_stage_connect_shm(struct llama_context * ctx, const char * name, int n_stages, int stage);
 LVK_API int lvk_stage_step(struct llama_context * ctx, const int * tokens, int n_tokens, int n_past, int greedy,
                            int micro);
 

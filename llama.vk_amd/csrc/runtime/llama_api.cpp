@@ -414,21 +414,39 @@ int lvk_rccl_unique_id(void * id, size_t n) {
     return 0;
 }
 
+// the checks every stage link makes before it joins its neighbours
+static void check_stage_position(llama_context * ctx, int n_stages, int stage) {
+    const lvk::Context & c = ctx->c;
+    if (ctx->split || n_stages < 1 || stage < 0 || stage >= n_stages) throw lvk::Error("bad stage link arguments");
+    if ((stage == 0) != c.model.has_embed || (stage == n_stages - 1) != c.model.has_head)
+        throw lvk::Error("the context's layer range does not match its stage position");
+}
+
 int lvk_stage_connect(struct llama_context * ctx, const void * id, int n_stages, int stage) {
     try {
-        lvk::Context & c = ctx->c;
-        if (ctx->split || n_stages < 1 || stage < 0 || stage >= n_stages || !id)
-            throw lvk::Error("bad stage link arguments");
-        if ((stage == 0) != c.model.has_embed || (stage == n_stages - 1) != c.model.has_head)
-            throw lvk::Error("the context's layer range does not match its stage position");
-        const lvk::Rccl & R = lvk::Rccl::get();
-        ncclUniqueId u;
-        std::memcpy(&u, id, sizeof(u));
+        check_stage_position(ctx, n_stages, stage);
+        if (!id) throw lvk::Error("bad stage link arguments");
         std::unique_ptr<lvk::StageLink, lvk::StageLinkDel> L(new lvk::StageLink);
         L->stage = stage;
         L->n_stages = n_stages;
-        lvk::DeviceGuard g(c.device);
-        R.check(R.CommInitRank(&L->comm, n_stages, u, stage), "ncclCommInitRank");
+        L->t = lvk::make_rccl_transport(id, n_stages, stage, ctx->c.device);
+        ctx->c.link = std::move(L);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());
+        return -1;
+    }
+    return 0;
+}
+
+int lvk_stage_connect_shm(struct llama_context * ctx, const char * name, int n_stages, int stage) {
+    try {
+        check_stage_position(ctx, n_stages, stage);
+        if (!name || !name[0]) throw lvk::Error("bad stage link arguments");
+        lvk::Context & c = ctx->c;
+        std::unique_ptr<lvk::StageLink, lvk::StageLinkDel> L(new lvk::StageLink);
+        L->stage = stage;
+        L->n_stages = n_stages;
+        L->t = lvk::make_shm_transport(name, n_stages, stage, (size_t) c.n_ctx * c.model.hp.n_embd * sizeof(float));
         c.link = std::move(L);
     } catch (const lvk::Error & e) {
         fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());

@@ -483,7 +483,7 @@ int Context::eval_greedy(int token, int n_past) {
     if (!model.has_head || !model.has_embed) throw Error("llama.vk_amd: greedy eval needs the whole model");
     EvalPart part;
     part.greedy = true;
-    begin_eval(&token, 1, n_past, part);
+    begin_eval_safe(&token, 1, n_past, part);
     end_eval(true);
     return *greedy_h;
 }
@@ -497,7 +497,7 @@ void Context::eval_sample(int token, int n_past) {
     if ((int) model.hp.n_vocab > SAMPLE_MAX_VOCAB) throw Error("llama.vk_amd: vocabulary too large for the device sampler");
     EvalPart part;
     part.sample = true;
-    begin_eval(&token, 1, n_past, part);
+    begin_eval_safe(&token, 1, n_past, part);
     end_eval(true);
 }
 
@@ -509,8 +509,22 @@ void Context::fetch_logits() {
 }
 
 void Context::eval(const int * tokens, int n, int n_past) {
-    begin_eval(tokens, n, n_past, EvalPart{});
+    begin_eval_safe(tokens, n, n_past, EvalPart{});
     end_eval(false);
+}
+
+// begin_eval for a caller that ends the eval itself: if the enqueue fails part-way, the
+// work already queued drains, the step blocks are released and the host logits are marked
+// stale before the error propagates (llama_get_logits then refuses them)
+void Context::begin_eval_safe(const int * tokens, int n, int n_past, const EvalPart & part) {
+    try {
+        begin_eval(tokens, n, n_past, part);
+    } catch (...) {
+        (void) hipStreamSynchronize(stream);
+        sp_next = 1;
+        logits_valid = false;
+        throw;
+    }
 }
 
 void Context::begin_eval(const int * tokens, int n, int n_past, const EvalPart & part) {

@@ -93,7 +93,7 @@ struct Context {
     unsigned * err_h = nullptr;  // pinned, mapped: the kernels' error word (lvk_kernels.h DevError)
     unsigned * err_d = nullptr;  // its device address
     int device = 0;              // the HIP device of this context
-    std::unique_ptr<StageLink, StageLinkDel> link;   // one-stage-per-process RCCL link (lvk_stage_connect)
+    std::unique_ptr<StageLink, StageLinkDel> link;   // one-stage-per-process link (lvk_stage_connect[_shm])
 
     // prompt (N > 1) path: MFMA matmuls with exact block dots (default) or the
     // bit-faithful VALU kernels (prompt_exact; env LVK_PROMPT_EXACT=1)
@@ -180,6 +180,7 @@ struct Context {
     // profile, device error word); a layer split interleaves the stages' begin_evals
     // with the residual-stream hand-offs and ends them together
     void begin_eval(const int * tokens, int n, int n_past, const EvalPart & part);
+    void begin_eval_safe(const int * tokens, int n, int n_past, const EvalPart & part);
     void end_eval(bool no_host_logits);
     // stage boundary: copy the residual stream x [n][E] to (to_ctx) or from the context
     void x_copy(void * buf, int n, bool to_ctx, bool on_device);

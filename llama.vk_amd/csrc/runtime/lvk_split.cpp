@@ -2,14 +2,28 @@
 #include "lvk_split.h"
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 
 namespace lvk {
 
 void SplitDel::operator()(Split * p) const { delete p; }
 void StageLinkDel::operator()(StageLink * p) const { delete p; }
+
+double stage_timeout_s() {
+    const char * e = getenv("LVK_STAGE_TIMEOUT_S");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0.0 ? v : 300.0;
+}
 
 DeviceGuard::DeviceGuard(int dev) {
     LVK_HIP(hipGetDevice(&prev));
@@ -20,11 +34,16 @@ DeviceGuard::~DeviceGuard() {
     if (hipGetDevice(&cur) == hipSuccess && cur != prev) (void) hipSetDevice(prev);
 }
 
-const Rccl & Rccl::get() {
-    static Rccl r;
+static std::string & rccl_err() {
     static std::string err;
+    return err;
+}
+
+static Rccl & rccl_load() {
+    static Rccl r;
     static std::once_flag once;
     std::call_once(once, [] {
+        std::string & err = rccl_err();
         void * h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
         if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
         if (!h) { err = std::string("cannot load librccl.so.1: ") + dlerror(); return; }
@@ -37,14 +56,26 @@ const Rccl & Rccl::get() {
         r.CommInitAll = (decltype(r.CommInitAll)) sym("ncclCommInitAll");
         r.CommInitRank = (decltype(r.CommInitRank)) sym("ncclCommInitRank");
         r.CommDestroy = (decltype(r.CommDestroy)) sym("ncclCommDestroy");
+        r.CommAbort = (decltype(r.CommAbort)) sym("ncclCommAbort");
+        r.CommGetAsyncError = (decltype(r.CommGetAsyncError)) sym("ncclCommGetAsyncError");
         r.Send = (decltype(r.Send)) sym("ncclSend");
         r.Recv = (decltype(r.Recv)) sym("ncclRecv");
         r.GroupStart = (decltype(r.GroupStart)) sym("ncclGroupStart");
         r.GroupEnd = (decltype(r.GroupEnd)) sym("ncclGroupEnd");
         r.GetErrorString = (decltype(r.GetErrorString)) sym("ncclGetErrorString");
     });
-    if (!err.empty()) throw Error("llama.vk_amd: " + err);
     return r;
+}
+
+const Rccl & Rccl::get() {
+    const Rccl & r = rccl_load();
+    if (!rccl_err().empty()) throw Error("llama.vk_amd: " + rccl_err());
+    return r;
+}
+
+bool Rccl::available() {
+    rccl_load();
+    return rccl_err().empty();
 }
 
 void Rccl::check(ncclResult_t res, const char * what) const {
@@ -73,6 +104,12 @@ void Split::connect(const char * transport) {
     if (t == "rccl" && !distinct) throw Error("llama.vk_amd: the rccl split transport needs one device per stage");
     if (t != "" && t != "rccl" && t != "copy") throw Error("llama.vk_amd: LVK_SPLIT_TRANSPORT must be rccl or copy");
     rccl = S > 1 && distinct && t != "copy";
+    if (rccl && t.empty() && !Rccl::available()) {
+        // no transport asked for and no librccl: the stream-ordered device copies work
+        // between distinct devices too (peer access or staged by the runtime)
+        fprintf(stderr, "llama.vk_amd: librccl.so.1 not loadable, the split hands off by device copies\n");
+        rccl = false;
+    }
     if (rccl) {
         const Rccl & R = Rccl::get();
         comms.assign(S, nullptr);
@@ -190,25 +227,204 @@ void Split::kv_set(const uint8_t * src, size_t n) {
     }
 }
 
+
 // ---------------------------------------------------------------------------
 // StageLink: one process per stage
 // ---------------------------------------------------------------------------
-StageLink::~StageLink() {
-    if (comm) (void) Rccl::get().CommDestroy(comm);
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+double since_s(Clock::time_point t0) { return std::chrono::duration<double>(Clock::now() - t0).count(); }
+
+// RCCL: ncclSend / ncclRecv on the stage stream; waits poll the stream and the
+// communicator's asynchronous error, and a failure or the time limit aborts the
+// communicator (its kernels stop, the peers' operations error out)
+struct RcclTransport final : StageTransport {
+    ncclComm_t comm = nullptr;
+    const char * name() const override { return "rccl"; }
+    ~RcclTransport() override {
+        if (comm) (void) Rccl::get().CommDestroy(comm);
+    }
+    void send(const void * d, size_t bytes, int peer, hipStream_t s) override {
+        const Rccl & R = Rccl::get();
+        if (!comm) throw Error("llama.vk_amd: stage link aborted");
+        R.check(R.Send(d, bytes, ncclInt8, peer, comm, s), "ncclSend");
+    }
+    void recv(void * d, size_t bytes, int peer, hipStream_t s) override {
+        const Rccl & R = Rccl::get();
+        if (!comm) throw Error("llama.vk_amd: stage link aborted");
+        R.check(R.Recv(d, bytes, ncclInt8, peer, comm, s), "ncclRecv");
+    }
+    void wait(hipStream_t s) override {
+        const Rccl & R = Rccl::get();
+        const double limit = stage_timeout_s();
+        const auto t0 = Clock::now();
+        for (int i = 0;; ++i) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) return;
+            if (q != hipErrorNotReady) LVK_HIP(q);
+            ncclResult_t ae = ncclSuccess;
+            if (comm && R.CommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                const std::string msg = std::string("llama.vk_amd: stage link RCCL error: ") + R.GetErrorString(ae);
+                abort();
+                throw Error(msg);
+            }
+            if (since_s(t0) > limit) {
+                abort();
+                throw Error("llama.vk_amd: stage step exceeded LVK_STAGE_TIMEOUT_S waiting for its neighbours");
+            }
+            if (i > 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+    }
+    void abort() noexcept override {
+        if (!comm) return;
+        (void) Rccl::get().CommAbort(comm);
+        comm = nullptr;
+    }
+};
+
+// Host shared-memory ring (POSIX shm, every stage opens the same name): ring s carries
+// stage s -> (s + 1) % S, so ring S-1 is the greedy relay from the last stage to the first.
+// The sender waits for its stream and copies the device buffer into the next free slot,
+// then publishes it; the receiver copies the slot into its device buffer on its stream and
+// frees the slot.  One abort word fails every stage's waits.
+constexpr int SHM_SLOTS = 2;
+struct ShmRing {
+    std::atomic<uint64_t> head;        // messages published (the sender writes)
+    std::atomic<uint64_t> tail;        // messages consumed (the receiver writes)
+    uint64_t bytes[SHM_SLOTS];
+};
+struct ShmHeader {
+    std::atomic<uint32_t> abort;
+    std::atomic<uint32_t> joined;
+    uint32_t n_stages;
+    uint32_t pad;
+    uint64_t slot_bytes;
+};
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory rings need address-free atomics");
+constexpr size_t SHM_DATA_OFF = 4096;
+
+struct ShmTransport final : StageTransport {
+    std::string shm_name;
+    int S = 1, stage = 0;
+    size_t slot = 0, total = 0;
+    uint8_t * base = nullptr;
+    ShmHeader * h = nullptr;
+    const char * name() const override { return "shm"; }
+    ShmRing * ring(int r) const { return (ShmRing *) (base + sizeof(ShmHeader)) + r; }
+    uint8_t * data(int r, uint64_t seq) const {
+        return base + SHM_DATA_OFF + ((size_t) r * SHM_SLOTS + (size_t) (seq % SHM_SLOTS)) * slot;
+    }
+    template <class F>
+    void spin_until(F ready, const char * what) {
+        const double limit = stage_timeout_s();
+        const auto t0 = Clock::now();
+        for (int i = 0; !ready(); ++i) {
+            if (h->abort.load(std::memory_order_acquire))
+                throw Error(std::string("llama.vk_amd: stage link aborted by a peer (") + what + ")");
+            if (since_s(t0) > limit) {
+                abort();
+                throw Error(std::string("llama.vk_amd: stage link timed out (") + what + ")");
+            }
+            if (i > 1024) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+    }
+    void open_ring(const char * nm, int n_stages, int st, size_t slot_bytes) {
+        shm_name = nm[0] == '/' ? nm : std::string("/") + nm;
+        S = n_stages;
+        stage = st;
+        slot = (slot_bytes + 4095) & ~(size_t) 4095;
+        total = SHM_DATA_OFF + (size_t) S * SHM_SLOTS * slot;
+        if (sizeof(ShmHeader) + (size_t) S * sizeof(ShmRing) > SHM_DATA_OFF) throw Error("llama.vk_amd: too many stages for the shm link");
+        const int fd = shm_open(shm_name.c_str(), O_CREAT | O_RDWR, 0600);
+        if (fd < 0) throw Error("llama.vk_amd: shm_open(" + shm_name + ") failed: " + strerror(errno));
+        // every stage sizes the object alike; a fresh object reads as zeros
+        if (ftruncate(fd, (off_t) total) != 0) {
+            const int e = errno;
+            close(fd);
+            throw Error("llama.vk_amd: ftruncate(" + shm_name + ") failed: " + strerror(e));
+        }
+        void * p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (p == MAP_FAILED) throw Error("llama.vk_amd: mmap of the shm link failed");
+        base = (uint8_t *) p;
+        h = (ShmHeader *) base;
+        // every stage must map the same object before any of them may unlink it
+        h->joined.fetch_add(1, std::memory_order_acq_rel);
+        spin_until([&] { return h->joined.load(std::memory_order_acquire) >= (uint32_t) S; }, "joining");
+    }
+    ~ShmTransport() override {
+        if (base) munmap(base, total);
+        if (stage == 0 && !shm_name.empty()) shm_unlink(shm_name.c_str());
+    }
+    void send(const void * d, size_t bytes, int peer, hipStream_t s) override {
+        if (peer != (stage + 1) % S || bytes > slot) throw Error("llama.vk_amd: bad shm link send");
+        ShmRing & r = *ring(stage);
+        const uint64_t seq = r.head.load(std::memory_order_relaxed);
+        LVK_HIP(hipStreamSynchronize(s));
+        spin_until([&] { return seq - r.tail.load(std::memory_order_acquire) < (uint64_t) SHM_SLOTS; }, "free slot");
+        LVK_HIP(hipMemcpy(data(stage, seq), d, bytes, hipMemcpyDeviceToHost));
+        r.bytes[seq % SHM_SLOTS] = bytes;
+        r.head.store(seq + 1, std::memory_order_release);
+    }
+    void recv(void * d, size_t bytes, int peer, hipStream_t s) override {
+        if (peer != (stage + S - 1) % S || bytes > slot) throw Error("llama.vk_amd: bad shm link recv");
+        ShmRing & r = *ring(peer);
+        const uint64_t seq = r.tail.load(std::memory_order_relaxed);
+        spin_until([&] { return r.head.load(std::memory_order_acquire) > seq; }, "message");
+        if (r.bytes[seq % SHM_SLOTS] != bytes) {
+            abort();
+            throw Error("llama.vk_amd: shm link message size differs between neighbouring stages");
+        }
+        LVK_HIP(hipMemcpyAsync(d, data(peer, seq), bytes, hipMemcpyHostToDevice, s));
+        LVK_HIP(hipStreamSynchronize(s));     // the slot is reused once tail moves
+        r.tail.store(seq + 1, std::memory_order_release);
+    }
+    void wait(hipStream_t s) override { LVK_HIP(hipStreamSynchronize(s)); }
+    void abort() noexcept override {
+        if (h) h->abort.store(1, std::memory_order_release);
+    }
+};
+
+}  // namespace
+
+std::unique_ptr<StageTransport> make_rccl_transport(const void * unique_id, int n_stages, int stage, int device) {
+    const Rccl & R = Rccl::get();
+    ncclUniqueId u;
+    std::memcpy(&u, unique_id, sizeof(u));
+    std::unique_ptr<RcclTransport> t(new RcclTransport);
+    DeviceGuard g(device);
+    R.check(R.CommInitRank(&t->comm, n_stages, u, stage), "ncclCommInitRank");
+    return t;
+}
+
+std::unique_ptr<StageTransport> make_shm_transport(const char * name, int n_stages, int stage, size_t slot_bytes) {
+    std::unique_ptr<ShmTransport> t(new ShmTransport);
+    t->open_ring(name, n_stages, stage, slot_bytes);
+    return t;
 }
 
 int stage_step(Context & c, const int * tokens, int n, int n_past, bool greedy, int micro) {
-    const Rccl & R = Rccl::get();
-    if (!c.link) throw Error("llama.vk_amd: stage not connected (lvk_stage_connect)");
+    if (!c.link || !c.link->t) throw Error("llama.vk_amd: stage not connected (lvk_stage_connect)");
     StageLink & L = *c.link;
+    StageTransport & T = *L.t;
     const int s = L.stage, S = L.n_stages;
-    if (greedy && n != 1) throw Error("llama.vk_amd: a greedy stage step takes one token");
-    if (n <= 0 || n_past < 0 || n_past + n > c.n_ctx_user) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
-    const int m = (micro > 0 && n > micro) ? micro : n;
     const size_t E = c.model.hp.n_embd;
-    DeviceGuard g(c.device);
+    const int V = (int) c.model.hp.n_vocab;
     std::string err;
+    DeviceGuard g(c.device);
     try {
+        // every argument is checked before the first transfer; a rank that fails anywhere in
+        // the step aborts the link, so its neighbours fail instead of waiting on it
+        if (greedy && n != 1) throw Error("llama.vk_amd: a greedy stage step takes one token");
+        if (n <= 0 || n_past < 0 || n_past + n > c.n_ctx_user) throw Error("llama.vk_amd: n_past + n_tokens exceeds n_ctx");
+        if (s == 0) {
+            if (!tokens) throw Error("llama.vk_amd: the first stage needs tokens");
+            for (int i = 0; i < n; ++i)
+                if (tokens[i] < 0 || tokens[i] >= V) throw Error("llama.vk_amd: token id out of range");
+        }
+        const int m = (micro > 0 && n > micro) ? micro : n;
         for (int off = 0; off < n; off += m) {
             const int k = std::min(m, n - off);
             EvalPart p;
@@ -217,28 +433,34 @@ int stage_step(Context & c, const int * tokens, int n, int n_past, bool greedy, 
             p.copy_out = off + k == n;
             p.head = p.copy_out || c.logits_all;
             p.greedy = greedy && s == S - 1;
-            if (s > 0) R.check(R.Recv(c.x, (size_t) k * E, ncclFloat32, s - 1, L.comm, c.stream), "ncclRecv");
+            if (s > 0) T.recv(c.x, (size_t) k * E * sizeof(float), s - 1, c.stream);
             c.begin_eval(s == 0 ? tokens + off : nullptr, k, n_past + off, p);
-            if (s + 1 < S) R.check(R.Send(c.x, (size_t) k * E, ncclFloat32, s + 1, L.comm, c.stream), "ncclSend");
+            if (s + 1 < S) T.send(c.x, (size_t) k * E * sizeof(float), s + 1, c.stream);
         }
         // greedy decode: the last stage's device argmax goes straight to the first stage,
         // whose host needs it to embed the next token
         if (greedy && S > 1) {
-            if (s == S - 1) R.check(R.Send(c.greedy_d, 1, ncclInt32, 0, L.comm, c.stream), "ncclSend");
+            if (s == S - 1) T.send(c.greedy_d, sizeof(int), 0, c.stream);
             if (s == 0) {
-                R.check(R.Recv(c.greedy_d, 1, ncclInt32, S - 1, L.comm, c.stream), "ncclRecv");
+                T.recv(c.greedy_d, sizeof(int), S - 1, c.stream);
                 LVK_HIP(hipMemcpyAsync(c.greedy_h, c.greedy_d, sizeof(int), hipMemcpyDeviceToHost, c.stream));
             }
         }
+        T.wait(c.stream);
     } catch (const Error & e) {
         err = e.msg;
+        T.abort();
     }
     try {
         c.end_eval(greedy && s == S - 1);
     } catch (const Error & e) {
         if (err.empty()) err = e.msg;
+        T.abort();
     }
-    if (!err.empty()) throw Error(err);
+    if (!err.empty()) {
+        c.logits_valid = false;
+        throw Error(err);
+    }
     return greedy && (s == 0 || s == S - 1) ? *c.greedy_h : 0;
 }
 

@@ -13,14 +13,19 @@
 //    waits between hops; prompts are cut into micro-batches that flow through the stages
 //    back to back (stage s runs micro-batch i+1 while stage s+1 runs i).  Stages that
 //    share a device (one-GPU rehearsal) hand off with a stream-ordered device copy.
-//  * StageLink -- one process per GPU (torchrun): lvk_stage_connect joins a
-//    ncclCommInitRank communicator of S ranks and lvk_stage_step does recv -> layers ->
-//    send on the rank's stream, plus the greedy token relay from the last stage to the
-//    first.
+//  * StageLink -- one process per stage: lvk_stage_connect joins a ncclCommInitRank
+//    communicator of S ranks (one GPU per rank), lvk_stage_connect_shm a host
+//    shared-memory ring (any placement, several stages on one GPU included); then
+//    lvk_stage_step does recv -> layers -> send on the rank's stream, plus the greedy token
+//    relay from the last stage to the first.  A rank that fails after its first transfer
+//    aborts the link (ncclCommAbort / the ring's abort word), so its peers fail instead of
+//    waiting forever, and every wait of a stage step is bounded (LVK_STAGE_TIMEOUT_S).
 #pragma once
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <memory>
+#include <string>
 
 #include "lvk_context.h"
 
@@ -33,12 +38,15 @@ struct Rccl {
     ncclResult_t (*CommInitAll)(ncclComm_t *, int, const int *) = nullptr;
     ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t *) = nullptr;
     ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
     const char * (*GetErrorString)(ncclResult_t) = nullptr;
     static const Rccl & get();   // throws lvk::Error when librccl cannot be loaded
+    static bool available();     // librccl loads (no throw)
     void check(ncclResult_t r, const char * what) const;
 };
 
@@ -73,11 +81,32 @@ struct Split {
     void kv_set(const uint8_t * src, size_t n);
 };
 
-struct StageLink {
-    ncclComm_t comm = nullptr;
-    int stage = 0, n_stages = 1;
-    ~StageLink();
+// The point-to-point transport of a one-process-per-stage link.  send/recv move `bytes`
+// between device buffers of neighbouring stages in the order of `stream` (RCCL: queued on
+// the stream; shm: the host waits for the stream, then copies through the ring).
+struct StageTransport {
+    virtual ~StageTransport() = default;
+    virtual const char * name() const = 0;
+    virtual void send(const void * d, size_t bytes, int peer, hipStream_t s) = 0;
+    virtual void recv(void * d, size_t bytes, int peer, hipStream_t s) = 0;
+    // wait for the stream with the link's health check and time limit; throws on failure
+    virtual void wait(hipStream_t s) = 0;
+    // make every peer's pending and future waits on this link fail (no throw)
+    virtual void abort() noexcept = 0;
 };
+
+struct StageLink {
+    std::unique_ptr<StageTransport> t;
+    int stage = 0, n_stages = 1;
+};
+
+// one RCCL communicator of S ranks (one GPU each)
+std::unique_ptr<StageTransport> make_rccl_transport(const void * unique_id, int n_stages, int stage, int device);
+// a POSIX shared-memory ring named `name` (every stage opens the same name); slot_bytes is
+// the largest message (n_ctx * n_embd * 4)
+std::unique_ptr<StageTransport> make_shm_transport(const char * name, int n_stages, int stage, size_t slot_bytes);
+// seconds a stage step may wait on its link (LVK_STAGE_TIMEOUT_S, default 300)
+double stage_timeout_s();
 
 // lvk_stage_step: one eval of this rank's stage between its neighbours; returns the next
 // greedy token on the first and last stage when greedy, else 0

@@ -15,6 +15,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LVK_LIB") or os.path.join(HERE, "lib", "libllama_vk_amd.so")
 GEN_BIN = os.path.join(HERE, "bin", "lvk-gen-model")
 
+# One HIP runtime per process: torch bundles its own libamdhip64 / libhsa-runtime64 /
+# librccl (ROCm 7.0, NEEDED as "libamdhip64.so"), this library links /opt/rocm's
+# (SONAME libamdhip64.so.7).  In one process the two either bind this library to torch's
+# runtime (torch imported first) or load both runtimes side by side (this library first),
+# which ended a round-2 test process in a glibc double free (profiles/r03_runtime_mix.md).
+# Keep torch in other processes (bench.py and the tests do); LVK_ALLOW_TORCH=1 overrides.
+if "torch" in __import__("sys").modules and os.environ.get("LVK_ALLOW_TORCH") != "1":
+    raise ImportError("llama.vk_amd: torch is already imported in this process; its bundled HIP runtime "
+                      "conflicts with this library's (run lvk in a process without torch, or set LVK_ALLOW_TORCH=1)")
 if not os.path.exists(LIB_PATH):
     raise ImportError("llama.vk_amd: %s not built (run __graft_entry__.build() or make -C llama.vk_amd)" % LIB_PATH)
 lib = C.CDLL(LIB_PATH)
@@ -113,6 +122,7 @@ _sig("lvk_stage_set_x", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_layers", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)])
 _sig("lvk_rccl_unique_id", C.c_int, [C.c_void_p, C.c_size_t])
 _sig("lvk_stage_connect", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
+_sig("lvk_stage_connect_shm", C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.c_int])
 _sig("lvk_stage_step", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int])
 _sig("lvk_init_split", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, i32p, C.c_char_p, C.c_int])
 _sig("lvk_split_info", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)])
@@ -207,6 +217,11 @@ class Llama:
         """join the RCCL communicator of a one-stage-per-process pipeline (lvk_stage_connect)"""
         buf = C.create_string_buffer(bytes(uid), 128)
         _check(lib.lvk_stage_connect(self.ctx, buf, int(n_stages), int(stage)), "lvk_stage_connect")
+
+    def stage_connect_shm(self, name, n_stages, stage):
+        """join a one-stage-per-process pipeline over a host shared-memory ring
+        (lvk_stage_connect_shm): returns once every stage has opened `name`"""
+        _check(lib.lvk_stage_connect_shm(self.ctx, name.encode(), int(n_stages), int(stage)), "lvk_stage_connect_shm")
 
     def stage_step(self, tokens, n_tokens, n_past, greedy=False, micro=64):
         """recv inpL -> this stage's layers -> send (lvk_stage_step); the greedy token on the

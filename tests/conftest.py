@@ -62,3 +62,11 @@ def gpu_available():
     if lvk.device_count() < 1:
         pytest.fail("no GPU visible to the gpu-marked test (HIP extension loaded, but no device)")
     return True
+
+
+def pytest_sessionfinish(session, exitstatus):
+    # one HIP runtime per process (lvk.py, profiles/r03_runtime_mix.md): a test that pulls
+    # torch into the process that loaded the library fails the session
+    if "lvk" in sys.modules and "torch" in sys.modules and os.environ.get("LVK_ALLOW_TORCH") != "1":
+        sys.stderr.write("\nERROR: torch was imported into the test process that loaded libllama_vk_amd.so\n")
+        session.exitstatus = 1
