@@ -330,4 +330,27 @@ hipError_t launch_rmsnorm_rows(const float * x, const float * g, int K, int n, f
 // greedy argmax over x[0..n) with the reference's first-maximum rule (llama.cpp:1382-1394); *out on the device
 // (out2, optional: a second copy of the token, e.g. host-mapped memory)
 hipError_t launch_argmax(const float * x, int n, int * out, hipStream_t s, int * out2 = nullptr);
+
+// ---------------------------------------------------------------------------
+// ggml graph operators (graph_ops.hip; include/ggml.h via runtime/ggml_graph.cpp): one
+// node per launch on a strided 4-D view of a device buffer
+enum GType : int { GT_Q4_0 = 0, GT_Q4_1 = 1, GT_I32 = 4, GT_F16 = 5, GT_F32 = 6 };   // = enum ggml_type
+enum GOp : int { GOP_ADD = 0, GOP_SUB, GOP_MUL, GOP_DIV, GOP_REPEAT, GOP_SCALE, GOP_SILU, GOP_DIAG_MASK };
+struct GView {
+    char * p = nullptr;
+    int64_t ne[4] = {1, 1, 1, 1};
+    int64_t nb[4] = {0, 0, 0, 0};
+    int type = GT_F32;
+};
+hipError_t launch_g_cpy(const GView & s, const GView & d, hipStream_t st);
+hipError_t launch_g_binary(const GView & a, const GView & b, const GView & d, int op, hipStream_t st);
+hipError_t launch_g_unary(const GView & s, const GView & d, int op, float v, int n_past, const uint16_t * tab,
+                          hipStream_t st);
+hipError_t launch_g_rms_norm(const GView & s, const GView & d, hipStream_t st);
+hipError_t launch_g_soft_max(const GView & d, const uint16_t * exp_tab, int exp_mode, hipStream_t st);
+hipError_t launch_g_rope(const GView & s, const GView & d, const float2 * cs, int n_dims, int i2_0, hipStream_t st);
+hipError_t launch_g_get_rows(const GView & s, const int32_t * idx, int64_t n_rows, const GView & d, hipStream_t st);
+// y: contiguous rows (f16 when s0 is f16, else f32) [ne13][ne12][ne11][ne00]
+hipError_t launch_g_mm_dot(const GView & s0, const void * y, int64_t ne11, const GView & d, hipStream_t st);
+
 }  // namespace lvk

@@ -61,7 +61,7 @@ struct CuParams {
 // the 64 and the per-row broadcast float4 reads are bank-conflict free
 constexpr int SRS = 40, SPL = 8 * SRS;
 
-template <int NW, int NP, int D, int PRO, int EPI, int KT>
+template <int NW, int NP, int D, int PRO, int EPI, int KT, bool PF>
 __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     constexpr int PT = NP * 64;                 // prologue threads
     constexpr int nb = KT / 32;                 // blocks per row
@@ -221,16 +221,26 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     const uint32_t loff = ng > 0 ? (uint32_t) lane * 16u : 0u;
     uint4 W[D][4];
     float4 S[D];
+    // the scales of a chunk go out before its nibbles: the scale table of chunk c+1 is
+    // built while chunk c's nibbles may still be in flight (vmcnt retires in order)
 #define LVK_ISSUE(slot, grp, cc)                                                                        \
     do {                                                                                                \
         const uint4 * nb_ = P.nib + ((size_t) (grp) * NC * 4 + (cc) * 4) * 64;                          \
+        S[slot] = *(const float4 *) ((const char *) (P.scl + ((size_t) (grp) * NC + (cc)) * 64) + loff); \
         _Pragma("unroll") for (int sb = 0; sb < 4; ++sb) if ((cc) * 4 + sb < nsub)                      \
             W[slot][sb] = ld_nt((const uint4 *) ((const char *) (nb_ + sb * 64) + loff));               \
-        S[slot] = *(const float4 *) ((const char *) (P.scl + ((size_t) (grp) * NC + (cc)) * 64) + loff); \
         __builtin_amdgcn_sched_barrier(0);                                                              \
     } while (0)
+    if constexpr (PF) {
+        // prologue first: the activation inputs land before this CU's weight burst is queued
+        // in front of them (every CU bursting at once delays a load issued behind the burst
+        // by the whole burst, MI355X_MICROARCH.md "prologue HBM burst")
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    LVK_T(58);
 #pragma unroll
     for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
+    LVK_T(59);
 
     if constexpr (NP == 0) {
         double * red = (double *) (sbuf + NW * 2 * SPL); // NW doubles (after the s buffers)
@@ -253,6 +263,7 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
                 acc = wave_sum_d(acc);
                 if (lane == 0) red[wave] = acc;
                 __syncthreads();
+                LVK_T(60);
                 double sum = red[0];
                 for (int w = 1; w < NW; ++w) sum += red[w];
                 const float mean = (float) (sum / (double) KT);
@@ -303,27 +314,37 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     LVK_T(2);
     if (NP == 0 && ng == 0) return;
 
-    // 4. row groups: chunk loop with cross-group prefetch
+    // 4. row groups: chunk loop with cross-group prefetch.  Per chunk: the chunk's
+    // activation words and scale products are read from LDS together up front (one exposed
+    // LDS latency per chunk instead of one per 4 blocks), the chains run, the slot is
+    // refilled, and the scale products of the NEXT chunk are written to the other table
+    // buffer (s = dw * dx, ggml.c:1968), so no write -> read round trip precedes a chain.
     float * sw = sbuf + wave * 2 * SPL;
+    int tbuf = 0;
+    auto make_table = [&](int buf, const float4 & Sv, int cc) __attribute__((always_inline)) {
+        const float4 dx = *(const float4 *) (dxp + cc * 32 + j * 4);
+        float4 sv;
+        sv.x = Sv.x * dx.x; sv.y = Sv.y * dx.y; sv.z = Sv.z * dx.z; sv.w = Sv.w * dx.w;
+        *(float4 *) (sw + buf * SPL + r * SRS + j * 4) = sv;
+    };
     auto body = [&](auto has_next, int grp, int gnext) __attribute__((always_inline)) {
         float acc = 0.0f;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             const int slot = c % D;
             LVK_T(tq); ++tq;
+            constexpr int NQ = 8;                   // 4-block activation groups per chunk
 #ifdef LVK_PROBE_NOCOMPUTE   // dev probe builds only: consume the weights trivially
             acc += __uint_as_float(W[slot][0].x ^ W[slot][nsub > 1 ? 1 : 0].y) * S[slot].x;
             if (false) {
 #else
             {
 #endif
-            float * sl = sw + (c & 1) * SPL;
-            // s = dw * dx of blocks 32c + 8m + j of row r (ggml.c:1968)
-            const float4 dx = *(const float4 *) (dxp + c * 32 + j * 4);
-            float4 sv;
-            sv.x = S[slot].x * dx.x; sv.y = S[slot].y * dx.y; sv.z = S[slot].z * dx.z; sv.w = S[slot].w * dx.w;
-            *(float4 *) (sl + r * SRS + j * 4) = sv;
-            __builtin_amdgcn_wave_barrier();
+            const float * sl = sw + tbuf * SPL;
+            uint4 A[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                if (c * 4 + q / 2 < nsub) A[q] = *(const uint4 *) (act + ((c * 8 + q) * 8 + j) * 4);
             float sa[8][4];
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
@@ -337,7 +358,7 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
 #pragma unroll
                     for (int pp = 0; pp < 2; ++pp) {
                         const int bi = sb * 8 + pp * 4;
-                        const uint4 a = *(const uint4 *) (act + ((c * 8 + sb * 2 + pp) * 8 + j) * 4);
+                        const uint4 a = A[sb * 2 + pp];
                         const int p0 = dot8(wd[2 * pp], a.x);
                         const int p1 = dot8(wd[2 * pp], a.y);
                         const int p2 = dot8(wd[2 * pp + 1], a.z);
@@ -352,6 +373,12 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
             }
             if (c + D < NC) LVK_ISSUE(slot, grp, c + D);
             else if constexpr (decltype(has_next)::value && XG) LVK_ISSUE(slot, gnext, c + D - NC);
+            // the next chunk's scale table: chunk c+1 of this group, or chunk 0 of the next
+            // (its scales sit in slot (c+1) % D either way)
+            if (c + 1 < NC) make_table(tbuf ^ 1, S[(c + 1) % D], c + 1);
+            else if constexpr (decltype(has_next)::value) make_table(tbuf ^ 1, S[(c + 1) % D], 0);
+            __builtin_amdgcn_wave_barrier();
+            tbuf ^= 1;
             // keep chunks in program order: the chain value is pinned here, so
             // chunk c's arithmetic cannot sink below chunk c+1's reads
             asm volatile("" : "+v"(acc));
@@ -398,6 +425,8 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
         }
     };
 
+    make_table(0, S[0], 0);                 // chunk 0 of the first group
+    __builtin_amdgcn_wave_barrier();
     if constexpr (XG) {
         for (int k = 0; k + 1 < ng; ++k) {
             const float res = body(std::true_type{}, gc, gc + NW);
@@ -596,6 +625,12 @@ __global__ __launch_bounds__(256) void k_mv_w2split(CuParams P) {
 
 // -- host -------------------------------------------------------------------
 
+// LVK_MV_PF=0 selects the weights-first prologue order (round-2 behaviour) for A/B runs
+static bool mv_pf() {
+    static const int v = [] { const char * e = getenv("LVK_MV_PF"); return e ? atoi(e) : 1; }();
+    return v != 0;
+}
+
 template <int NW, int NP, int D, int PRO, int EPI, int KT>
 hipError_t go(const CuParams & P, hipStream_t s) {
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
@@ -604,7 +639,8 @@ hipError_t go(const CuParams & P, hipStream_t s) {
     // without cross-group prefetch every wave must own at most one group
     if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
     const size_t lds = (size_t) nb * 32 + NC * 128 + NW * 2 * SPL * 4 + NW * 8;
-    LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
+    if (mv_pf()) LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, true>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
+    else LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, false>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
     return hipGetLastError();
 }
 
@@ -686,7 +722,7 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         switch (epi) {
             case EPI_QKV: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_QKV, 8192>(P, s); break;
             case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 8192>(P, s); break;
-            case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 8192>(P, s); break;
+            case EPI_STORE: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_STORE, 8192>(P, s); break;
             case EPI_RESID: if (pro == PRO_ACTQ) return go<4, 0, 2, PRO_ACTQ, EPI_RESID, 8192>(P, s); break;
         }
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 8192>(P, s);

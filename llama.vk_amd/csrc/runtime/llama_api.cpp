@@ -656,18 +656,62 @@ const char * llama_print_system_info(void) {
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
-// include/ggml.h: the ggml calls of the reference example programs
+// include/llama_internal.h: the model file's tensors by name (reference llama.cpp:1850-1852)
 // ---------------------------------------------------------------------------
-#include "../../../include/ggml.h"
+#include <fcntl.h>
 
-struct ggml_context { int unused; };
+#include "../../../include/llama_internal.h"
 
-static int64_t g_t0_us = 0;
-void ggml_time_init(void) { g_t0_us = lvk::now_us(); }
-int64_t ggml_time_ms(void) { return (lvk::now_us() - g_t0_us) / 1000; }
-int64_t ggml_time_us(void) { return lvk::now_us() - g_t0_us; }
-struct ggml_context * ggml_init(struct ggml_init_params params) {
-    (void) params;
-    return new ggml_context{0};
+namespace {
+struct TensorMap {
+    void * addr = nullptr;
+    size_t size = 0;
+    std::vector<ggml_tensor> tensors;
+    std::vector<std::pair<std::string, ggml_tensor *>> by_name;
+    ~TensorMap() {
+        if (addr && size) munmap(addr, size);
+    }
+};
+}  // namespace
+
+std::vector<std::pair<std::string, struct ggml_tensor *>> & llama_internal_get_tensor_map(struct llama_context * ctx) {
+    static std::vector<std::pair<std::string, struct ggml_tensor *>> empty;
+    if (ctx->tensor_map) return static_cast<TensorMap *>(ctx->tensor_map.get())->by_name;
+    try {
+        const lvk::Model & m = ctx->c.model;
+        size_t fsize = 0;
+        const std::vector<lvk::FileTensor> list = lvk::file_tensor_list(m.path, fsize);
+        std::shared_ptr<TensorMap> tm = std::make_shared<TensorMap>();
+        const int fd = open(m.path.c_str(), O_RDONLY);
+        if (fd < 0) throw lvk::Error("cannot open " + m.path);
+        tm->addr = mmap(nullptr, fsize, PROT_READ, MAP_SHARED, fd, 0);
+        close(fd);
+        if (tm->addr == MAP_FAILED) {
+            tm->addr = nullptr;
+            throw lvk::Error("mmap failed for " + m.path);
+        }
+        tm->size = fsize;
+        tm->tensors.resize(list.size());
+        for (size_t i = 0; i < list.size(); ++i) {
+            const lvk::FileTensor & f = list[i];
+            ggml_tensor & t = tm->tensors[i];
+            std::memset(&t, 0, sizeof t);
+            // ggjt type ids 0 f32, 1 f16, 2 q4_0, 3 q4_1 (llama.cpp:387-395) -> enum ggml_type
+            t.type = f.type == 0 ? GGML_TYPE_F32 : f.type == 1 ? GGML_TYPE_F16 : f.type == 2 ? GGML_TYPE_Q4_0 : GGML_TYPE_Q4_1;
+            t.n_dims = (int) f.ne.size();
+            for (int d = 0; d < GGML_MAX_DIMS; ++d) t.ne[d] = d < t.n_dims ? f.ne[d] : 1;
+            t.nb[0] = ggml_type_size(t.type);
+            t.nb[1] = t.nb[0] * (t.ne[0] / ggml_blck_size(t.type));
+            for (int d = 2; d < GGML_MAX_DIMS; ++d) t.nb[d] = t.nb[d - 1] * t.ne[d - 1];
+            t.op = GGML_OP_NONE;
+            t.data = (char *) tm->addr + f.off;
+            tm->by_name.emplace_back(f.name, &t);
+        }
+        ctx->tensor_map = tm;
+        return tm->by_name;
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());
+        empty.clear();
+        return empty;
+    }
 }
-void ggml_free(struct ggml_context * ctx) { delete ctx; }

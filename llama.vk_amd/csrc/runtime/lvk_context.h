@@ -210,6 +210,7 @@ void host_fp16_tables(std::vector<uint16_t> & exp_tab, std::vector<uint16_t> & s
 struct llama_context {
     lvk::Context c;                                  // the whole model, or the last stage of a split
     std::unique_ptr<lvk::Split, lvk::SplitDel> split;   // layer split over devices (lvk_split.h)
+    std::shared_ptr<void> tensor_map;                // llama_internal_get_tensor_map's state (on first use)
     // every stage context in layer order (just &c without a split)
     std::vector<lvk::Context *> stages();
 };

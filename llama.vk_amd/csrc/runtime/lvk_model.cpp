@@ -120,7 +120,8 @@ FileInfo read_header(Reader & rd, Vocab * vocab) {
     return fi;
 }
 
-void read_tensor_index(Reader & rd, FileVer ver, size_t file_idx, std::map<std::string, std::vector<Shard>> & idx) {
+void read_tensor_index(Reader & rd, FileVer ver, size_t file_idx, std::map<std::string, std::vector<Shard>> & idx,
+                       std::vector<FileTensor> * order = nullptr) {
     while (rd.off < rd.n) {
         Shard sh;
         const uint32_t nd = rd.u32();
@@ -136,6 +137,7 @@ void read_tensor_index(Reader & rd, FileVer ver, size_t file_idx, std::map<std::
         sh.size = type_row_bytes(sh.type, sh.ne[0]) * rows;
         if (rd.off + sh.size > rd.n) throw Error("tensor '" + name + "' data is not within the file bounds");
         rd.off += sh.size;
+        if (order) order->push_back({name, sh.type, sh.ne, sh.off, sh.size});
         idx[name].push_back(sh);
     }
 }
@@ -168,6 +170,7 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
     Reader rd{files[0]->p(), files[0]->size};
     FileInfo fi = read_header(rd, &m.vocab);
     m.hp = fi.hp;
+    m.path = path;
     if (vocab_only) return;
 
     std::map<std::string, std::vector<Shard>> idx;
@@ -361,6 +364,21 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
         tick(w2.size);
     }
     m.load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+}
+
+// the tensor directory of a single-part model file in file order (llama_internal_get_tensor_map)
+std::vector<FileTensor> file_tensor_list(const std::string & path, size_t & file_size) {
+    MappedFile f(path);
+    Reader rd{f.p(), f.size};
+    FileInfo fi = read_header(rd, nullptr);
+    std::map<std::string, std::vector<Shard>> idx;
+    std::vector<FileTensor> order;
+    read_tensor_index(rd, fi.ver, 0, idx, &order);
+    auto te = idx.find("tok_embeddings.weight");
+    if (te != idx.end() && fi.hp.n_embd != te->second.at(0).ne.at(0))
+        throw Error("the tensor map of a multi-part model file is not supported");
+    file_size = f.size;
+    return order;
 }
 
 }  // namespace lvk

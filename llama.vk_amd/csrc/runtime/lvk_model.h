@@ -66,11 +66,21 @@ struct Model {
     std::vector<DevBuf> bufs;      // owned device memory
     size_t weight_bytes = 0;       // bytes of weights resident in HBM (quad-sliced images)
     size_t file_bytes = 0;
+    std::string path;              // the model file (llama_internal_get_tensor_map re-maps it)
     double load_ms = 0;
 
     void * alloc(size_t n);
     ~Model();
 };
+
+// one tensor of a model file: ggjt type id, ne (ne[0] = row length), data offset and bytes
+struct FileTensor {
+    std::string name;
+    uint32_t type = 0;
+    std::vector<uint32_t> ne;
+    size_t off = 0, size = 0;
+};
+std::vector<FileTensor> file_tensor_list(const std::string & path, size_t & file_size);
 
 // Load a ggjt v1 (or ggmf/ggml vocab-only) file.  vocab_only stops after the
 // vocabulary.  layer_end < 0 means all layers; a partial range [layer_begin,

@@ -26,11 +26,11 @@ def lvk():
 
 def declared_symbols():
     syms = []
-    for h in ("llama.h", "lvk_ops.h"):
+    for h in ("llama.h", "lvk_ops.h", "ggml.h"):
         txt = open(os.path.join(ROOT, "include", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         txt = "\n".join(ln for ln in txt.splitlines() if not ln.lstrip().startswith("#"))
-        for m in re.finditer(r"(?:LLAMA_API|LVK_API)\s+[^;(]*?\b(\w+)\s*\(", txt):
+        for m in re.finditer(r"(?:LLAMA_API|LVK_API|LVK_GGML_API)\s+[^;(]*?\b(\w+)\s*\(", txt):
             syms.append(m.group(1))
     return syms
 
@@ -42,6 +42,9 @@ def test_exports_every_declared_symbol(lvk):
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     missing = [s for s in syms if s not in exported]
     assert not missing, missing
+    # include/llama_internal.h: the one C++ entry point (reference llama_internal.h:104)
+    out = subprocess.check_output(["nm", "-DC", "--defined-only", LIB]).decode()
+    assert "llama_internal_get_tensor_map[abi:cxx11](llama_context*)" in out
 
 
 def test_reference_llama_api_symbols_present(lvk):

@@ -1,7 +1,8 @@
 """The reference's own example programs, unmodified, linked to this library.
 
 tools/dropin/Makefile compiles /root/reference/examples/{main,perplexity,
-embedding,quantize} against include/llama.h (+ include/ggml.h) and links them
+embedding,quantize,quantize-stats} against include/llama.h (+ include/ggml.h,
+include/llama_internal.h) and links them
 to libllama_vk_amd.so instead of the reference's llama.o/ggml.o -- the drop-in
 boundary of INTEGRATION.md.  The reference CPU build of the same main
 (oracle/_ref/main) is the checker: with greedy sampling, bit-exact logits give
@@ -135,3 +136,44 @@ def test_dropin_perplexity_matches_reference_cpu(tiny_models, tmp_path):
     assert _ppl_values(exact_out) == want        # bit-exact logits -> the same printed digits
     mfma_out, _ = _run([exe] + args + ["-t", "1"])
     assert _ppl_values(mfma_out) == want         # the MFMA prompt path is bit-exact too
+
+
+@pytest.mark.gpu
+def test_dropin_embedding_matches_reference_cpu(tiny_models):
+    """examples/embedding (embedding.cpp:81-90: the last token's normed embedding printed
+    with %f) on the GPU library vs the reference build: the same printed vector"""
+    exe = os.path.join(DROPIN, "embedding")
+    ref_exe = os.path.join(ROOT, "oracle", "_ref", "embedding")
+    _need(exe)
+    _need(ref_exe)
+    args = ["-m", tiny_models["tiny_q4_0"], "-p", "Building a website can be done in 10 simple steps:",
+            "-c", "128", "-s", "1"]
+    gpu_out, _ = _run([exe] + args + ["-t", "1"])
+    cpu_out, _ = _run([ref_exe] + args + ["-t", "8"])
+    vals = gpu_out.split()
+    assert len(vals) == 256
+    assert gpu_out == cpu_out
+
+
+def _qstats_lines(out):
+    # everything but the wall-clock line (quantize-stats.cpp:346-351)
+    return [l for l in out.decode().splitlines() if "time" not in l]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [["-l", "norm", "-p"], ["-l", "norm", "-r", "--histogram", "-t", "q4_1"]])
+def test_dropin_quantize_stats_matches_reference_cpu(tiny_models, flags):
+    """examples/quantize-stats, unmodified, on this library: llama_internal_get_tensor_map
+    (the file's tensors by name) + ggml_internal_get_quantize_fn (quantize / dequantize on the
+    GPU) print the same per-layer and total error statistics as the reference build (the
+    float tensors of a Q4 file: the norms)"""
+    exe = os.path.join(DROPIN, "quantize-stats")
+    ref_exe = os.path.join(ROOT, "oracle", "_ref", "quantize-stats")
+    _need(exe)
+    _need(ref_exe)
+    args = ["-m", tiny_models["tiny_q4_0"]] + flags
+    gpu_out, _ = _run([exe] + args)
+    cpu_out, _ = _run([ref_exe] + args)
+    got, want = _qstats_lines(gpu_out), _qstats_lines(cpu_out)
+    assert len(want) >= 4
+    assert got == want

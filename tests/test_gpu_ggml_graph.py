@@ -1,0 +1,36 @@
+"""ggml_graph_compute on the GPU against the reference ggml.c: one ggml caller
+(tools/ggml_graph/graph_test.c) builds the LLaMA graph of llama_eval_internal
+(reference llama.cpp:927-1197: get_rows, rms_norm, mul/repeat, Q4 mul_mat, reshape, rope,
+cpy into the KV views, permute, f16/f32 mul_mat, scale, diag_mask_inf, soft_max, add, silu)
+for a 7-token prompt, a 33-token batch and two decode steps, computes it with this library
+(every node on the GPU) and with the reference's CPU AVX2 ggml.c, and both dumps -- logits of
+every step and both KV caches -- must be bit-identical.  Weights Q4_0 or Q4_1, KV f16 or f32."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from test_ggml_graph import LVK_BIN, REF_BIN, _build
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wtype,kv", [(0, 1), (1, 1), (0, 0)])
+def test_graph_compute_matches_reference_ggml(gpu_available, wtype, kv, tmp_path):
+    _build()
+    if not os.path.exists(REF_BIN):
+        pytest.skip("reference build oracle/_ref/graph_test_ref not present")
+    dumps = []
+    for b, name in ((REF_BIN, "ref"), (LVK_BIN, "lvk")):
+        out = tmp_path / ("%s.bin" % name)
+        r = subprocess.run([b, str(out), str(wtype), str(kv)], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        dumps.append(np.fromfile(out, np.uint8))
+    assert dumps[0].size == dumps[1].size and dumps[0].size > 0
+    V = 512
+    n_logits = V * (7 + 33 + 1 + 1)
+    a = dumps[0][:n_logits * 4].view(np.float32)
+    b = dumps[1][:n_logits * 4].view(np.float32)
+    bad = np.flatnonzero(a.view(np.uint32) != b.view(np.uint32))
+    assert bad.size == 0, "logits differ at %d places, first %s: %r vs %r" % (bad.size, bad[:5], a[bad[:5]], b[bad[:5]])
+    assert np.array_equal(dumps[0], dumps[1]), "KV caches differ"

@@ -288,6 +288,18 @@ int main(int argc, char ** argv) {
         }
         printf("trace kind %s: %d compute waves; avg cycles from entry: staged-seen %.0f act-ready %.0f end %.0f (max end %.0f)\n",
                names[kind], nw, sum_issue / nw, sum_pro / nw, sum_end / nw, maxend);
+        {
+            double a[3] = {0, 0, 0}; int c[3] = {0, 0, 0};
+            double first_entry = 1e30, last_entry = 0;
+            for (int w = 0; w < 256 * 16; w++) {
+                unsigned long long * e = &h[(size_t) w * 64];
+                if (!e[0] || !e[3]) continue;
+                first_entry = std::min(first_entry, (double) e[0]); last_entry = std::max(last_entry, (double) e[0]);
+                for (int q = 0; q < 3; q++) if (e[58 + q]) { a[q] += e[58 + q] - e[0]; c[q]++; }
+            }
+            printf("  inputs-landed %.0f  weights-issued %.0f  norm-synced %.0f  (entry spread %.0f cycles)\n",
+                   c[0] ? a[0] / c[0] : -1.0, c[1] ? a[1] / c[1] : -1.0, c[2] ? a[2] / c[2] : -1.0, last_entry - first_entry);
+        }
         printf("  (loader waves %d) staged-issued %.0f  first-publish %.0f  end %.0f\n", npw, pe[0] / std::max(1, npw), pe[1] / std::max(1, npw), pe[2] / std::max(1, npw));
         for (int c = 0; c < 26 && cn[c]; c++)
             printf("  chunk %2d: n %5d  gap-before %6.0f  body %6.0f\n", c, cn[c], cw[c] / cn[c], cs[c] / cn[c]);
