@@ -59,15 +59,19 @@ __global__ void k_g_binary(GView a, GView b, GView d, int op) {
     for (int64_t k = blockIdx.x * (int64_t) blockDim.x + threadIdx.x; k < n; k += (int64_t) gridDim.x * blockDim.x) {
         int64_t i0, i1, i2, i3;
         unflatten(k, d.ne, i0, i1, i2, i3);
-        const float x = *(const float *) at(a, i0, i1, i2, i3);
-        float y = 0.0f, r;
-        if (op != GOP_REPEAT) y = *(const float *) at(b, i0, i1, i2, i3);
-        switch (op) {
-            case GOP_ADD: r = x + y; break;
-            case GOP_SUB: r = x - y; break;
-            case GOP_MUL: r = x * y; break;
-            case GOP_DIV: r = x / y; break;
-            default: r = *(const float *) at(a, i0 % a.ne[0], i1 % a.ne[1], i2 % a.ne[2], i3 % a.ne[3]); break;
+        float r;
+        if (op == GOP_REPEAT) {
+            // a is smaller than d: index it modulo its own shape only
+            r = *(const float *) at(a, i0 % a.ne[0], i1 % a.ne[1], i2 % a.ne[2], i3 % a.ne[3]);
+        } else {
+            const float x = *(const float *) at(a, i0, i1, i2, i3);
+            const float y = *(const float *) at(b, i0, i1, i2, i3);
+            switch (op) {
+                case GOP_ADD: r = x + y; break;
+                case GOP_SUB: r = x - y; break;
+                case GOP_MUL: r = x * y; break;
+                default: r = x / y; break;
+            }
         }
         *(float *) at(d, i0, i1, i2, i3) = r;
     }
@@ -178,6 +182,7 @@ __global__ void k_g_rope(GView s, GView d, const float2 * cs, int n_dims, int i2
 __global__ void k_g_get_rows(GView s, const int32_t * idx, GView d) {
     const int64_t r = blockIdx.y;
     const int64_t row = idx[r];
+    if (row < 0 || row >= s.ne[1]) return;     // (the host rejects such ids of a leaf index tensor)
     const char * src = s.p + row * s.nb[1];
     for (int64_t i0 = blockIdx.x * (int64_t) blockDim.x + threadIdx.x; i0 < d.ne[0]; i0 += (int64_t) gridDim.x * blockDim.x) {
         float v;

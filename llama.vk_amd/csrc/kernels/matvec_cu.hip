@@ -61,7 +61,7 @@ struct CuParams {
 // the 64 and the per-row broadcast float4 reads are bank-conflict free
 constexpr int SRS = 40, SPL = 8 * SRS;
 
-template <int NW, int NP, int D, int PRO, int EPI, int KT, bool PF>
+template <int NW, int NP, int D, int PRO, int EPI, int KT, int PF>
 __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     constexpr int PT = NP * 64;                 // prologue threads
     constexpr int nb = KT / 32;                 // blocks per row
@@ -216,9 +216,8 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     }
 
     // first D chunks of this wave's first row group (wave-uniform base +
-    // 32-bit lane offset: the scalar-base load form).  A wave without row
-    // groups (NP == 0 only) aims its loads at one 16-byte word.
-    const uint32_t loff = ng > 0 ? (uint32_t) lane * 16u : 0u;
+    // 32-bit lane offset: the scalar-base load form)
+    const uint32_t loff = (uint32_t) lane * 16u;
     uint4 W[D][4];
     float4 S[D];
     // the scales of a chunk go out before its nibbles: the scale table of chunk c+1 is
@@ -231,15 +230,23 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
             W[slot][sb] = ld_nt((const uint4 *) ((const char *) (nb_ + sb * 64) + loff));               \
         __builtin_amdgcn_sched_barrier(0);                                                              \
     } while (0)
-    if constexpr (PF) {
-        // prologue first: the activation inputs land before this CU's weight burst is queued
-        // in front of them (every CU bursting at once delays a load issued behind the burst
-        // by the whole burst, MI355X_MICROARCH.md "prologue HBM burst")
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // Order of the prologue and the first weight loads (PF):
+    //   0: weights first, then the activation table (the inputs land behind the burst);
+    //   1: the inputs land, then the weights are issued, then the table is built;
+    //   2: the inputs land and the table is built, then the weights are issued.
+    // A CU's texture unit takes a 1 KiB wave load in ~16 cycles: issuing 80-160 KiB of
+    // weights keeps every wave of the CU in its issue for 1.3-4k cycles, so with 0 or 1 the
+    // table (and the first chain) waits for the whole burst to be issued (tools/probe traces).
+    if constexpr (PF >= 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     LVK_T(58);
+    // a wave without row groups issues no weight loads (it only helps build the table)
+    const bool issue = NP > 0 || ng > 0;
+    if constexpr (PF <= 1) {
+        if (issue) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
+            for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
+        }
+    }
     LVK_T(59);
 
     if constexpr (NP == 0) {
@@ -307,6 +314,12 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
                     act_store(act, dxp, b, 3, qv[k].w, 0.0f, false);
                 }
             }
+        }
+    }
+    if constexpr (PF == 2) {
+        if (issue) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
         }
     }
     LVK_T(1);
@@ -625,10 +638,10 @@ __global__ __launch_bounds__(256) void k_mv_w2split(CuParams P) {
 
 // -- host -------------------------------------------------------------------
 
-// LVK_MV_PF=0 selects the weights-first prologue order (round-2 behaviour) for A/B runs
-static bool mv_pf() {
-    static const int v = [] { const char * e = getenv("LVK_MV_PF"); return e ? atoi(e) : 1; }();
-    return v != 0;
+// prologue order (k_mv_cu PF); LVK_MV_PF=0/1/2 overrides for A/B runs
+static int mv_pf() {
+    static const int v = [] { const char * e = getenv("LVK_MV_PF"); return e ? atoi(e) : 2; }();
+    return v;
 }
 
 template <int NW, int NP, int D, int PRO, int EPI, int KT>
@@ -639,8 +652,11 @@ hipError_t go(const CuParams & P, hipStream_t s) {
     // without cross-group prefetch every wave must own at most one group
     if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
     const size_t lds = (size_t) nb * 32 + NC * 128 + NW * 2 * SPL * 4 + NW * 8;
-    if (mv_pf()) LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, true>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
-    else LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, false>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
+    switch (mv_pf()) {
+        case 0: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 0>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
+        case 1: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 1>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
+        default: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 2>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
+    }
     return hipGetLastError();
 }
 
@@ -699,11 +715,11 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         switch (cfg) { case 0: return go<a0, PR, E, K_>(P, s); case 1: return go<a1, PR, E, K_>(P, s); \
                        case 2: return go<a2, PR, E, K_>(P, s); default: return go<a3, PR, E, K_>(P, s); }
 #define C3(a, b, c) a, b, c
-        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(8, 0, 4), C3(6, 0, 4), C3(12, 0, 4))
-        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(12, 0, 4), C3(16, 0, 2), C3(16, 0, 4))
-        if (K == 4096 && epi == EPI_STORE) SW4(EPI_STORE, PRO_NORM, 4096, C3(16, 0, 2), C3(8, 0, 4), C3(12, 0, 2), C3(8, 4, 2))
-        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 0, 4), C3(4, 0, 4), C3(4, 0, 2))
-        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(4, 0, 4), C3(4, 0, 11), C3(2, 0, 11), C3(4, 0, 8))
+        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(8, 0, 1), C3(12, 0, 1), C3(6, 0, 2))
+        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(12, 0, 1), C3(16, 0, 1), C3(8, 0, 2))
+        if (K == 4096 && epi == EPI_STORE) SW4(EPI_STORE, PRO_NORM, 4096, C3(16, 0, 2), C3(16, 0, 1), C3(12, 0, 2), C3(12, 0, 1))
+        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 0, 4), C3(2, 0, 1), C3(4, 0, 2))
+        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(4, 0, 4), C3(2, 0, 4), C3(2, 0, 11), C3(8, 0, 4))
     }
 #endif
     // launch shapes (waves NW, prefetch depth D) per row length and role, measured on

@@ -569,8 +569,11 @@ namespace {
 
 // bytes a strided tensor spans from its data pointer
 size_t span_bytes(const ggml_tensor * t) {
-    size_t s = (size_t) (t->ne[0] / BLCK_SIZE[t->type]) * TYPE_SIZE[t->type];
-    for (int d = 1; d < GGML_MAX_DIMS; ++d)
+    // quantized rows are contiguous blocks; other types may have any stride in any
+    // dimension (a transpose swaps nb[0] and nb[1])
+    const bool quant = BLCK_SIZE[t->type] > 1;
+    size_t s = quant ? (size_t) (t->ne[0] / BLCK_SIZE[t->type]) * TYPE_SIZE[t->type] : TYPE_SIZE[t->type];
+    for (int d = quant ? 1 : 0; d < GGML_MAX_DIMS; ++d)
         if (t->ne[d] > 1) s += (size_t) (t->ne[d] - 1) * t->nb[d];
     return s;
 }
@@ -692,6 +695,7 @@ void run_mul_mat_q(GraphRun & R, const ggml_tensor * a, const ggml_tensor * b, g
             lvk::StepParams sp{0, N, 0, 0};
             lvk::StepParams * spd = (lvk::StepParams *) R.temp(sizeof sp);
             LVK_HIP(hipMemcpyAsync(spd, &sp, sizeof sp, hipMemcpyHostToDevice, R.stream));
+            LVK_HIP(hipStreamSynchronize(R.stream));      // sp is this scope's host memory
             lvk::MvLaunch L;
             L.w = q; L.sp = spd; L.n_tokens = N; L.y = y;
             if (qt == lvk::Q4_1) {
@@ -803,6 +807,11 @@ void run_node(GraphRun & R, ggml_tensor * n) {
             G_ASSERT(b->type == GGML_TYPE_I32 && n->type == GGML_TYPE_F32);
             G_ASSERT(a->type == GGML_TYPE_Q4_0 || a->type == GGML_TYPE_Q4_1 || a->type == GGML_TYPE_F16 ||
                      a->type == GGML_TYPE_F32);
+            if (b->op == GGML_OP_NONE)
+                for (int64_t i = 0; i < b->ne[0]; ++i) {
+                    const int32_t id = ((const int32_t *) b->data)[i];
+                    if (id < 0 || id >= a->ne[1]) gabort("ggml_get_rows: row index out of range");
+                }
             LVK_HIP(lvk::launch_g_get_rows(R.view(a), (const int32_t *) R.dev(b->data), b->ne[0], R.view(n), R.stream));
             return;
         case GGML_OP_MUL_MAT:
@@ -859,10 +868,21 @@ extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph
             LVK_HIP(hipMalloc(&r.dev, (size_t) (r.hi - r.lo) + 16));
             LVK_HIP(hipMemcpyAsync(r.dev, r.lo, (size_t) (r.hi - r.lo), hipMemcpyHostToDevice, R.stream));
         }
+        // LVK_GGML_SYNC=1: wait for every node and name the one that fails (debugging)
+        static const bool sync_each = getenv("LVK_GGML_SYNC") && atoi(getenv("LVK_GGML_SYNC")) != 0;
         for (int i = 0; i < cgraph->n_nodes; ++i) {
             ggml_tensor * n = cgraph->nodes[i];
             run_node(R, n);
             if (n->op != GGML_OP_NONE) R.region_of(n->data).written = true;
+            if (sync_each) {
+                const hipError_t e = hipStreamSynchronize(R.stream);
+                if (e != hipSuccess) {
+                    fprintf(stderr, "ggml_graph_compute: node %d (op %d, type %d, ne %lld %lld %lld %lld) failed: %s\n", i,
+                            (int) n->op, (int) n->type, (long long) n->ne[0], (long long) n->ne[1], (long long) n->ne[2],
+                            (long long) n->ne[3], hipGetErrorString(e));
+                    abort();
+                }
+            }
         }
         for (Region & r : R.regions)
             if (r.written) LVK_HIP(hipMemcpyAsync(r.lo, r.dev, (size_t) (r.hi - r.lo), hipMemcpyDeviceToHost, R.stream));
