@@ -126,11 +126,13 @@ struct AttnDArgs {
     float * out_f32;
     int exp_mode;
     unsigned * err;               // host-mapped error word (nullptr: none)
+    int short_max;                // n_kv <= short_max: no score exchange (every workgroup scores all)
 };
 
 // EXCH: the 4 workgroups of a head split the scores and exchange them as granules;
-// !EXCH: every workgroup scores all positions itself (4x the K reads, from the XCD's L2)
-template <int QT, bool EXCH = true>
+// !EXCH: every workgroup scores all positions itself (4x the K reads, from the XCD's L2).
+// DYN: the choice is made per launch from n_kv (exchange only above A.short_max).
+template <int QT, bool EXCH = true, bool DYN = false>
 __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, const int sl, uint8_t * smem) {
     const int E = A.E, n_ctx = A.n_ctx, d0 = h * HD + sl * 32;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = tid & 3;
@@ -139,39 +141,55 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     uint16_t * pl = (uint16_t *) (sc + n_ctx);                   // [n_ctx]
     float * red = (float *) (pl + n_ctx);                        // 8 floats
     double * redd = (double *) (red + 8);                        // 4 doubles
-    u64g * g = (u64g *) (A.gran + (size_t) h * n_ctx);
+    u64g * g = (u64g * ) (A.gran + (size_t) h * n_ctx);
     LVK_DT(0);
 
-    // 1a. Q and the step block go out together (one memory round trip); every K and V
-    // load is bounded by n_kv, so a launch reads exactly the positions it uses
+    // 1a. Loads that do not depend on n_past go out before the step block is read: Q,
+    // the K rows of positions 0..63 (chunk 0; rows past n_kv are read, never used) and the
+    // V slice of positions 0..63.  A short context (n_kv <= 64, no exchange) then has all
+    // its operands in flight from the first cycle.
     const uint4 * qp = (const uint4 *) (A.q16 + h * HD) + r;
     uint4 qv[4];
 #pragma unroll
     for (int st = 0; st < 4; ++st) qv[st] = qp[st * 4];
-    const int n_kv = A.sp->n_past + 1;
-    const int n_pad = (n_kv + 31) & ~31;
-    const int np = n_kv & ~31;
-    auto v_dma = [&](int p0, int lim) {             // positions [p0, p0 + 512) of the 32 rows, below lim
+    auto v_dma = [&](int p0, int lo, int lim) {     // positions [max(p0, lo), min(p0 + 512, lim)) of the 32 rows
         for (int row = wave; row < 32; row += 4)
-            if (p0 + lane * 8 < lim)
+            if (p0 + lane * 8 >= lo && p0 + lane * 8 < lim)
                 __builtin_amdgcn_global_load_lds((const void *) (A.vc + (size_t) (d0 + row) * n_ctx + p0 + lane * 8),
                                                  (__attribute__((address_space(3))) void *) (vl + (size_t) row * n_ctx + p0),
                                                  16, 0, 0);
     };
     uint4 kv[2][4];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const int p = min((EXCH ? sl * 64 + c * 256 : c * 64) + (tid >> 2), n_kv - 1);
+    {
+        const int p = min(tid >> 2, n_ctx - 1);
         const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
 #pragma unroll
-        for (int st = 0; st < 4; ++st) kv[c][st] = kp[st * 4];
+        for (int st = 0; st < 4; ++st) kv[0][st] = kp[st * 4];
+    }
+    v_dma(0, 0, 64);
+    const int n_kv = A.sp->n_past + 1;
+    const int n_pad = (n_kv + 31) & ~31;
+    const int np = n_kv & ~31;
+    const bool exch = DYN ? n_kv > A.short_max : EXCH;
+    // the rest of this workgroup's first two K chunks
+    {
+        const bool c0_other = exch && sl > 0;                    // chunk 0 of an exchange is position sl*64+
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (c == 0 && !c0_other) continue;
+            const int base = exch ? sl * 64 + c * 256 : c * 64;
+            const int p = min(base + (tid >> 2), n_kv - 1);
+            const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) kv[c][st] = kp[st * 4];
+        }
     }
     LVK_DT(6);
-    for (int p0 = 0; p0 < n_pad; p0 += 512) v_dma(p0, n_pad);
+    for (int p0 = 0; p0 < n_pad; p0 += 512) v_dma(p0, 64, n_pad);
     LVK_DT(7);
     LVK_DT(1);
 
-    // 1b. scores of chunks sl, sl+4, ... (one position per lane quad)
+    // 1b. scores of chunks sl, sl+4, ... (exchange) or of every chunk (one position per lane quad)
     {
         float qf[4][8];
 #pragma unroll
@@ -188,7 +206,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
             const float kq = quad_reduce(s);
             if (r == 0 && p < n_kv) {
                 const float v = kq * A.scale;                    // ggml_vec_scale_f32 (llama.cpp:1026)
-                if constexpr (!EXCH) sc[p] = v;
+                if (!exch) sc[p] = v;
 #ifdef LVK_PROBE_DROP_GRANULE   // fault-injection probe build only: position 0's score is never published
                 else if (p == 0) {}
 #endif
@@ -196,8 +214,8 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
         };
-        const int cs = EXCH ? 256 : 64;                     // position stride of this workgroup's chunks
-        const int cb = EXCH ? sl * 64 : 0;
+        const int cs = exch ? 256 : 64;                     // position stride of this workgroup's chunks
+        const int cb = exch ? sl * 64 : 0;
 #pragma unroll
         for (int c = 0; c < 2; ++c)
             if (cb + c * cs < n_kv) score(kv[c], cb + c * cs + (tid >> 2));
@@ -213,9 +231,9 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     LVK_DT(2);
     // 2. every score of the head: poll each granule until it carries this layer's epoch
     float mx = -INFINITY;
-    if constexpr (!EXCH) __syncthreads();
+    if (!exch) __syncthreads();
     for (int p = tid; p < n_kv; p += 256) {
-        const float v = EXCH ? __uint_as_float((unsigned) poll_granule(g + p, A.epoch, A.err)) : sc[p];
+        const float v = exch ? __uint_as_float((unsigned) poll_granule(g + p, A.epoch, A.err)) : sc[p];
         sc[p] = v;
         mx = v > mx ? v : mx;
     }
@@ -340,7 +358,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
 template <int QT, bool EXCH>
 __global__ __launch_bounds__(256) void k_attn_d(AttnDArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    attn_d_run<QT, EXCH>(A, blockIdx.x, blockIdx.y, smem);
+    attn_d_run<QT, EXCH, true>(A, blockIdx.x, blockIdx.y, smem);
 }
 
 // ---- k_attn_wo: the Wo workgroups (row length n_embd = 4096 compiled in) ----
@@ -533,6 +551,14 @@ AttnDArgs attn_args(const AttnLaunch & A, void * gran, unsigned epoch) {
     a.out_f32 = A.out_f32;
     a.exp_mode = A.exp_computed;
     a.err = A.err;
+    // short contexts skip the score exchange: every workgroup of a head scores all n_kv
+    // positions itself (tools/probe: cheaper than the cross-workgroup hand-off up to ~128)
+    static const int short_max = [] {
+        const char * e = getenv("LVK_ATTN_SHORT");
+        if (getenv("LVK_ATTN_NOEXCH") && atoi(getenv("LVK_ATTN_NOEXCH")) != 0) return 1 << 30;
+        return e ? atoi(e) : 64;
+    }();
+    a.short_max = short_max;
     return a;
 }
 

@@ -210,8 +210,8 @@ __global__ void k_g_get_rows(GView s, const int32_t * idx, GView d) {
 // mul_mat f16 x f32 (ggml.c:6299-6487): src1 already converted to contiguous f16 rows
 // (the INIT phase, RNE), then dst[ic][i01] = ggml_vec_dot_f16 (ggml.c:1781-1815): 4 x 8
 // fp32 FMA accumulators over n & ~31, the F32Cx8 reduce, the tail in double.  Also
-// f32 x f32 (ggml_vec_dot_f32, ggml.c:1713-1748: same accumulators and reduce, tail
-// fmaf in float) when s0.type == GT_F32 (y then f32 contiguous rows).
+// f32 x f32 (ggml_vec_dot_f32, ggml.c:1713-1748: same accumulators and reduce, the tail
+// summed in float) when s0.type == GT_F32 (y then f32 contiguous rows).
 __global__ void k_g_mm_dot(GView s0, const void * y, int64_t ne11, GView d) {
     const int64_t n = s0.ne[0];
     const int64_t total = s0.ne[1] * ne11 * s0.ne[2] * s0.ne[3];
@@ -256,8 +256,12 @@ __global__ void k_g_mm_dot(GView s0, const void * y, int64_t ne11, GView d) {
             }
             out = (float) sumf;
         } else {
+            // the reference is built as ISO C (-std=c11: no contraction): product, then sum
             float sumf = res;
-            for (int64_t i = np; i < n; ++i) sumf = __builtin_fmaf(xv(i), yv(i), sumf);
+            for (int64_t i = np; i < n; ++i) {
+                const float p = xv(i) * yv(i);
+                sumf = sumf + p;
+            }
             out = sumf;
         }
         *(float *) at(d, i01, ic, i02, i03) = out;

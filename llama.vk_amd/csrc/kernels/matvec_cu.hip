@@ -233,7 +233,8 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     // Order of the prologue and the first weight loads (PF):
     //   0: weights first, then the activation table (the inputs land behind the burst);
     //   1: the inputs land, then the weights are issued, then the table is built;
-    //   2: the inputs land and the table is built, then the weights are issued.
+    //   2: the inputs land and the table is built, then the weights are issued;
+    //   3: as 2, but the weights are issued after the workgroup barrier.
     // A CU's texture unit takes a 1 KiB wave load in ~16 cycles: issuing 80-160 KiB of
     // weights keeps every wave of the CU in its issue for 1.3-4k cycles, so with 0 or 1 the
     // table (and the first chain) waits for the whole burst to be issued (tools/probe traces).
@@ -326,6 +327,12 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     __syncthreads();            // activation table ready
     LVK_T(2);
     if (NP == 0 && ng == 0) return;
+    if constexpr (PF == 3) {
+        // 3: the table first, then every wave issues its own weights and starts its chain
+        // as soon as they land (no workgroup barrier behind the issue)
+#pragma unroll
+        for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
+    }
 
     // 4. row groups: chunk loop with cross-group prefetch.  Per chunk: the chunk's
     // activation words and scale products are read from LDS together up front (one exposed
@@ -453,198 +460,16 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
 #undef LVK_ISSUE
 }
 
-// ---------------------------------------------------------------------------
-// W2 with each row group's blocks split over two waves (opt-in, LVK_W2_SPLIT=1; Q4_0,
-// f32 input quantized in the prologue, residual epilogue).  The chain order is the only
-// order-bound part of ggml_vec_dot_q4_0: wave part 0 runs the fp32 chains over the first
-// H sub-chunks as k_mv_cu does, wave part 1 computes the integer partials (int16) and
-// block scales of the rest into LDS in parallel, and part 0 then continues the same
-// chains through them in block order -- bit-identical, with the CU's second SIMD pair
-// doing half of the dot/convert work and all weight loads of a wave issued at once
-// (static counts: K is a template constant, the loops are fully unrolled).
-// ---------------------------------------------------------------------------
-#ifndef LVK_W2S_H
-#define LVK_W2S_H 26         // sub-chunks of part 0 of 43 (22: 10.5 us, 26: 9.9, 30: 10.0; 0: half)
-#endif
-template <int KT>
-__global__ __launch_bounds__(256) void k_mv_w2split(CuParams P) {
-    constexpr int NW = 4, RG = 2;               // 2 row groups x 2 parts per workgroup
-    constexpr int nb = KT / 32, nsub = nb / 8, NC = (nb + 31) / 32;
-    constexpr int H = LVK_W2S_H > 0 ? LVK_W2S_H : (nsub + 1) / 2;   // sub-chunks of part 0
-    constexpr int NS1 = nsub - H;               // sub-chunks of part 1
-    constexpr int NB1 = NS1 * 8;                // blocks of part 1
-    constexpr int C0 = (H * 4 + 15) / 16;       // chunks part 0 touches (sub-chunk s -> chunk s / 4)
-    constexpr int CA1 = H / 4, CB1 = (nsub - 1) / 4;   // chunk range of part 1
-    constexpr int NC1 = CB1 - CA1 + 1;
-    constexpr int nunits = KT / 8;
-    constexpr int NT = NW * 64;
-    constexpr int UM = (nunits + NT - 1) / NT;
-    static_assert(nb % 8 == 0, "K must be a multiple of 256");
-
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t * act = (uint32_t *) smem;                          // nb * 32 B
-    float * dxp = (float *) (smem + nb * 32);                    // NC * 128 B
-    float * sbuf = dxp + NC * 32;                                // NW * 2 * SPL floats
-    constexpr int PST = NB1 + 4;                                 // lane row stride (floats, 16-byte aligned)
-    float * p1 = sbuf + NW * 2 * SPL;                            // [RG][64 lanes][PST] partials as f32
-    float * s1 = p1 + RG * 64 * PST;                             // [RG][8 rows][NB1] block scales
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int rg = wave >> 1, part = wave & 1;
-    const int j = lane & 7, r = lane >> 3;
-    const int nwg = gridDim.x;
-    const int g0 = (int) (blockIdx.x * (unsigned) P.G / (unsigned) nwg);
-    const int g1 = (int) ((blockIdx.x + 1) * (unsigned) P.G / (unsigned) nwg);
-    const int grp = g0 + rg;
-    const bool live = grp < g1;
-    const int gl = live ? grp : g0;             // a dead wave aims its loads at a live group
-
-    // prologue inputs first (vmcnt retires in order), then every weight load of this wave
-    float4 xv[UM][2];
-#pragma unroll
-    for (int k = 0; k < UM; ++k) {
-        const int un = min(k * NT + tid, nunits - 1);
-        const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
-        xv[k][0] = xp[0]; xv[k][1] = xp[1];
-    }
-    const uint32_t loff = (uint32_t) lane * 16u;
-    auto wsub = [&](int sidx) -> uint4 {
-        const int c = sidx >> 2, sb = sidx & 3;
-        return ld_nt((const uint4 *) ((const char *) (P.nib + ((size_t) gl * NC * 4 + c * 4 + sb) * 64) + loff));
-    };
-    auto wscl = [&](int c) -> float4 {
-        return *(const float4 *) ((const char *) (P.scl + ((size_t) gl * NC + c) * 64) + loff);
-    };
-    constexpr int NCW = C0 > NC1 ? C0 : NC1;
-#ifndef LVK_W2S_RING
-#define LVK_W2S_RING 4
-#endif
-    constexpr int RING = LVK_W2S_RING;          // sub-chunks in flight per wave (all: 13.5 us, 12: 11.7, 8: 11.2, 4: 10.5, 2: 11.1)
-    uint4 W[RING];
-    float4 S[NCW];
-    const int sbase = part == 0 ? 0 : H;
-    const int scount = part == 0 ? H : NS1;
-#pragma unroll
-    for (int i = 0; i < RING; ++i)
-        if (i < scount) W[i] = wsub(sbase + i);
-    if (part == 0) {
-#pragma unroll
-        for (int c = 0; c < C0; ++c) S[c] = wscl(c);
-    } else {
-#pragma unroll
-        for (int c = 0; c < NC1; ++c) S[c] = wscl(CA1 + c);
-    }
-
-    // activation table: quantize_row_q4_0 of the f32 input (as k_mv_cu PRO_ACTF)
-#pragma unroll
-    for (int k = 0; k < UM; ++k) {
-        if (k * NT >= nunits) break;
-        const int un = k * NT + tid;
-        float v[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w, xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
-        float amax = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { const float a = fabsf(v[e]); amax = a > amax ? a : amax; }
-        const float o0 = quad_bcast<0>(amax), o1 = quad_bcast<1>(amax);
-        const float o2 = quad_bcast<2>(amax), o3 = quad_bcast<3>(amax);
-        const float m01 = o1 > o0 ? o1 : o0, m23 = o3 > o2 ? o3 : o2;
-        amax = m23 > m01 ? m23 : m01;
-        const float d = amax / 7.0f;                              // ggml.c:651
-        const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;     // ggml.c:653
-        const uint32_t w = q40_pack8(v, id);
-        if (un < nunits) act_store(act, dxp, un >> 2, un & 3, w, d, (un & 3) == 0);
-    }
-    __syncthreads();            // activation table ready
-
-    float * sw = sbuf + wave * 2 * SPL;
-    // block scales s = dw * dx of chunk c for this lane's row (ggml.c:1968), via the wave's table
-    auto scales = [&](int c, const float4 & Sc, float (&sa)[8][4]) __attribute__((always_inline)) {
-        float * sl = sw + (c & 1) * SPL;
-        const float4 dx = *(const float4 *) (dxp + c * 32 + j * 4);
-        float4 sv;
-        sv.x = Sc.x * dx.x; sv.y = Sc.y * dx.y; sv.z = Sc.z * dx.z; sv.w = Sc.w * dx.w;
-        *(float4 *) (sl + r * SRS + j * 4) = sv;
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-            const float4 v = *(const float4 *) (sl + r * SRS + jj * 4);
-            sa[jj][0] = v.x; sa[jj][1] = v.y; sa[jj][2] = v.z; sa[jj][3] = v.w;
-        }
-    };
-    float acc = 0.0f;
-    if (live && part == 0) {
-        float sa[8][4];
-#pragma unroll
-        for (int i = 0; i < H; ++i) {
-            const int c = i >> 2, sb = i & 3;
-            if (sb == 0) scales(c, S[c], sa);
-            const uint32_t wd[4] = {W[i % RING].x, W[i % RING].y, W[i % RING].z, W[i % RING].w};
-            if (i + RING < H) W[i % RING] = wsub(i + RING);
-#pragma unroll
-            for (int pp = 0; pp < 2; ++pp) {
-                const int bi = sb * 8 + pp * 4;
-                const uint4 a = *(const uint4 *) (act + ((c * 8 + sb * 2 + pp) * 8 + j) * 4);
-                const int q0 = dot8(wd[2 * pp], a.x), q1 = dot8(wd[2 * pp], a.y);
-                const int q2 = dot8(wd[2 * pp + 1], a.z), q3 = dot8(wd[2 * pp + 1], a.w);
-                acc = __builtin_fmaf(sa[(bi + 0) & 7][(bi + 0) >> 3], (float) q0, acc);
-                acc = __builtin_fmaf(sa[(bi + 1) & 7][(bi + 1) >> 3], (float) q1, acc);
-                acc = __builtin_fmaf(sa[(bi + 2) & 7][(bi + 2) >> 3], (float) q2, acc);
-                acc = __builtin_fmaf(sa[(bi + 3) & 7][(bi + 3) >> 3], (float) q3, acc);
-            }
-            asm volatile("" : "+v"(acc));
-        }
-    } else if (live) {
-        // part 1: integer partials and scales of sub-chunks H.. into LDS, block order
-        float * pw = p1 + ((size_t) rg * 64 + lane) * PST;
-        float * sw1 = s1 + ((size_t) rg * 8 + r) * NB1;
-        float sa[8][4];
-#pragma unroll
-        for (int i = 0; i < NS1; ++i) {
-            const int si = H + i, c = si >> 2, sb = si & 3;
-            if (i == 0 || sb == 0) scales(c, S[c - CA1], sa);
-            const uint32_t wd[4] = {W[i % RING].x, W[i % RING].y, W[i % RING].z, W[i % RING].w};
-            if (i + RING < NS1) W[i % RING] = wsub(H + i + RING);
-#pragma unroll
-            for (int pp = 0; pp < 2; ++pp) {
-                const int bi = sb * 8 + pp * 4;
-                const uint4 a = *(const uint4 *) (act + ((c * 8 + sb * 2 + pp) * 8 + j) * 4);
-                const int bl = i * 8 + pp * 4;                    // first of the 4 blocks within part 1
-                *(float4 *) (pw + bl) = make_float4((float) dot8(wd[2 * pp], a.x), (float) dot8(wd[2 * pp], a.y),
-                                                    (float) dot8(wd[2 * pp + 1], a.z), (float) dot8(wd[2 * pp + 1], a.w));
-                if (j == 0)
-                    *(float4 *) (sw1 + bl) = make_float4(sa[(bi + 0) & 7][(bi + 0) >> 3], sa[(bi + 1) & 7][(bi + 1) >> 3],
-                                                         sa[(bi + 2) & 7][(bi + 2) >> 3], sa[(bi + 3) & 7][(bi + 3) >> 3]);
-            }
-        }
-    }
-    __syncthreads();            // part 1's partials and scales are in LDS
-    if (!live || part != 0) return;
-    {
-        const float * pw = p1 + ((size_t) rg * 64 + lane) * PST;
-        const float * sw1 = s1 + ((size_t) rg * 8 + r) * NB1;
-#pragma unroll 6
-        for (int bl = 0; bl < NB1; bl += 4) {
-            const float4 pv = *(const float4 *) (pw + bl), sv = *(const float4 *) (sw1 + bl);
-            acc = __builtin_fmaf(sv.x, pv.x, acc);       // ggml.c:2013, blocks in order
-            acc = __builtin_fmaf(sv.y, pv.y, acc);
-            acc = __builtin_fmaf(sv.z, pv.z, acc);
-            acc = __builtin_fmaf(sv.w, pv.w, acc);
-        }
-    }
-    const float res = octet_reduce(acc);
-    const int row = grp * 8 + r;
-    if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1103)
-}
-
 // -- host -------------------------------------------------------------------
 
-// prologue order (k_mv_cu PF); LVK_MV_PF=0/1/2 overrides for A/B runs
-static int mv_pf() {
-    static const int v = [] { const char * e = getenv("LVK_MV_PF"); return e ? atoi(e) : 2; }();
+// prologue order (k_mv_cu PF): PFD per launch shape (measured, tools/probe sweeps);
+// LVK_MV_PF=0..3 overrides it for A/B runs
+static int mv_pf_env() {
+    static const int v = [] { const char * e = getenv("LVK_MV_PF"); return e ? atoi(e) : -1; }();
     return v;
 }
 
-template <int NW, int NP, int D, int PRO, int EPI, int KT>
+template <int NW, int NP, int D, int PRO, int EPI, int KT, int PFD = 2>
 hipError_t go(const CuParams & P, hipStream_t s) {
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
     constexpr bool XG = (NC % D) == 0;
@@ -652,10 +477,12 @@ hipError_t go(const CuParams & P, hipStream_t s) {
     // without cross-group prefetch every wave must own at most one group
     if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
     const size_t lds = (size_t) nb * 32 + NC * 128 + NW * 2 * SPL * 4 + NW * 8;
-    switch (mv_pf()) {
+    const int pf = mv_pf_env() >= 0 ? mv_pf_env() : PFD;
+    switch (pf) {
         case 0: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 0>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
         case 1: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 1>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
-        default: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 2>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
+        case 2: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 2>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
+        default: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 3>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
     }
     return hipGetLastError();
 }
@@ -684,12 +511,6 @@ bool matvec_cu_supported(int K, int qtype) {
     return K == 4096 || K == 11008 || K == 8192 || K == 22016;
 }
 
-// LVK_W2_SPLIT=1: the 11008-long residual matvec (W2) on k_mv_w2split
-static bool w2_split_env() {
-    const char * e = getenv("LVK_W2_SPLIT");
-    return e && atoi(e) != 0;
-}
-
 hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s) {
     if (L.w.qtype == Q4_1) return launch_matvec_cu41(L, pro, epi, s);
     if (L.w.qtype != Q4_0 || L.n_tokens != 1 || L.w.M % 8) return hipErrorNotSupported;
@@ -715,11 +536,11 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         switch (cfg) { case 0: return go<a0, PR, E, K_>(P, s); case 1: return go<a1, PR, E, K_>(P, s); \
                        case 2: return go<a2, PR, E, K_>(P, s); default: return go<a3, PR, E, K_>(P, s); }
 #define C3(a, b, c) a, b, c
-        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(8, 0, 1), C3(12, 0, 1), C3(6, 0, 2))
-        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(12, 0, 1), C3(16, 0, 1), C3(8, 0, 2))
-        if (K == 4096 && epi == EPI_STORE) SW4(EPI_STORE, PRO_NORM, 4096, C3(16, 0, 2), C3(16, 0, 1), C3(12, 0, 2), C3(12, 0, 1))
-        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 0, 4), C3(2, 0, 1), C3(4, 0, 2))
-        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(4, 0, 4), C3(2, 0, 4), C3(2, 0, 11), C3(8, 0, 4))
+        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(8, 0, 3), C3(8, 0, 4), C3(12, 0, 2))
+        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(12, 0, 3), C3(12, 0, 4), C3(16, 0, 2))
+        if (K == 4096 && epi == EPI_STORE) SW4(EPI_STORE, PRO_NORM, 4096, C3(16, 0, 2), C3(16, 0, 3), C3(12, 0, 2), C3(12, 0, 3))
+        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 0, 4), C3(4, 0, 2), C3(8, 0, 2))
+        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(4, 0, 4), C3(8, 0, 4), C3(16, 0, 4), C3(8, 0, 6))
     }
 #endif
     // launch shapes (waves NW, prefetch depth D) per row length and role, measured on
@@ -727,10 +548,10 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
     // every CU keeps ~60-120 KB of weights in flight
     if (K == 4096) {
         switch (epi) {
-            case EPI_QKV: if (pro == PRO_NORM) return go<8, 0, 2, PRO_NORM, EPI_QKV, 4096>(P, s); break;
-            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 4096>(P, s); break;
-            case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 4096>(P, s); break;
-            case EPI_RESID: if (pro == PRO_ACTQ) return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096>(P, s); break;
+            case EPI_QKV: if (pro == PRO_NORM) return go<8, 0, 2, PRO_NORM, EPI_QKV, 4096, 2>(P, s); break;
+            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 4096, 1>(P, s); break;
+            case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 4096, 1>(P, s); break;
+            case EPI_RESID: if (pro == PRO_ACTQ) return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096, 2>(P, s); break;
         }
         // operator API (lvk_mul_mat_q: plain quantize of an f32 input)
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 4096>(P, s);
@@ -743,14 +564,8 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         }
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 8192>(P, s);
     } else if (K == 11008) {
-        if (epi == EPI_RESID && pro == PRO_ACTF && w2_split_env() && (P.G + cu_count() - 1) / cu_count() <= 2) {
-            constexpr int nb = 11008 / 32, nsub = nb / 8, NC = (nb + 31) / 32;
-            constexpr int NB1 = (nsub - (LVK_W2S_H > 0 ? LVK_W2S_H : (nsub + 1) / 2)) * 8;
-            const size_t lds = (size_t) nb * 32 + NC * 128 + 4 * 2 * SPL * 4 + 2 * 64 * (NB1 + 4) * 4 + 2 * NB1 * 8 * 4;
-            LVK_LAUNCH(k_mv_w2split<11008>, dim3(std::min(cu_count(), P.G)), dim3(256), lds, s, P);
-            return hipGetLastError();
-        }
-        if (epi == EPI_RESID && pro == PRO_ACTF) return go<4, 0, 4, PRO_ACTF, EPI_RESID, 11008>(P, s);
+        // 8 waves: the 6 without a row group help quantize u (tools/probe sweep r03: 8.0 vs 8.9 us)
+        if (epi == EPI_RESID && pro == PRO_ACTF) return go<8, 0, 4, PRO_ACTF, EPI_RESID, 11008, 2>(P, s);
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 0, 4, PRO_ACTF, EPI_STORE, 11008>(P, s);
         if (epi == EPI_STORE && pro == PRO_NORM) return go<4, 0, 4, PRO_NORM, EPI_STORE, 11008>(P, s);
     } else if (K == 22016) {

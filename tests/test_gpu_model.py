@@ -127,30 +127,6 @@ def test_7b_shaped_decode_vs_oracle(lvk, oracle, model_dir):
     om.close()
 
 
-def test_7b_shaped_decode_w2_split_matches(lvk, oracle, model_dir, monkeypatch):
-    """The parked split-chain W2 kernel (k_mv_w2split, LVK_W2_SPLIT=1: a second wave computes
-    the integer partials of the later blocks into LDS, the owning wave runs the chains through
-    them in block order) stays bit-identical to the oracle over 12 decode positions."""
-    from oracle_lib import gen_model
-    path = gen_model(os.path.join(model_dir, "w4096_l2.bin"), n_embd=4096, n_head=32, n_layer=2, ftype=2, seed=7)
-    monkeypatch.setenv("LVK_W2_SPLIT", "1")
-    m = lvk.Llama(path, n_ctx=512)
-    om = oracle.model(path, 512)
-    toks = np.array([1, 450, 4996, 17354, 1701, 29916, 338, 263], np.int32)
-    a = m.eval(toks, 0)
-    b = om.eval(toks, 0)
-    assert np.array_equal(bits(a), bits(b))
-    n_past, tok = len(toks), int(np.argmax(a[-1]))
-    for _ in range(12):
-        a = m.eval([tok], n_past)
-        b = om.eval([tok], n_past)
-        assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past
-        n_past += 1
-        tok = int(np.argmax(a[-1]))
-    m.close()
-    om.close()
-
-
 def test_7b_shaped_fused_attention_wo_matches(lvk, oracle, model_dir, monkeypatch):
     """The opt-in one-launch attention + Wo (k_attn_wo, LVK_FUSE_ATTN_WO=1) on LLaMA-7B
     layer shapes: decode logits bit-identical to the oracle across 40 positions."""

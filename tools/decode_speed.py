@@ -42,7 +42,7 @@ def main():
     m.close()
     ks = {k: round(v['ms'] / v['launches'] * 1e3, 2) for k, v in p.items() if v['launches']}
     gbs = {k: round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 0) for k, v in p.items() if v['launches'] and v.get('bytes')}
-    print(json.dumps({'model': name, 'lib': os.environ.get('LVK_LIB', 'default'), 'cfg41': os.environ.get('LVK_CFG41'), 'w2split': os.environ.get('LVK_W2_SPLIT', '0'),
+    print(json.dumps({'model': name, 'lib': os.environ.get('LVK_LIB', 'default'), 'cfg41': os.environ.get('LVK_CFG41'),
                       'tok_s': round(1 / dt, 1), 'ms_per_token': round(dt * 1e3, 3), 'kernels_us': ks, 'gbs': gbs}),
           flush=True)
 
