@@ -186,6 +186,9 @@ LVK_API int lvk_stage_connect(struct llama_context * ctx, const void * id, int n
 /* The same link through a host shared-memory ring (POSIX shm object `name`, opened by every
  * stage): any stage placement, several stages on one GPU included, no RCCL.  The call
  * returns once all n_stages stages have opened the ring. */
+/* 1 when this build carries the parked kernels (lib/dev: the persistent decode kernel,
+ * the fused attention + Wo launch), 0 for the product library */
+LVK_API int lvk_dev_kernels(void);
 LVK_API int lvk_stage_connect_shm(struct llama_context * ctx, const char * name, int n_stages, int stage);
 LVK_API int lvk_stage_step(struct llama_context * ctx, const int * tokens, int n_tokens, int n_past, int greedy,
                            int micro);

@@ -361,6 +361,7 @@ __global__ __launch_bounds__(256) void k_attn_d(AttnDArgs A) {
     attn_d_run<QT, EXCH, true>(A, blockIdx.x, blockIdx.y, smem);
 }
 
+#ifdef LVK_DEV_KERNELS   // parked (measured slower than two launches): lib/dev only
 // ---- k_attn_wo: the Wo workgroups (row length n_embd = 4096 compiled in) ----
 namespace wo {
 constexpr int KT = 4096;
@@ -518,6 +519,7 @@ __global__ __launch_bounds__(256) void k_attn_wo(AttnDArgs A, WoArgs P) {
     if (b < nattn) attn_d_run<Q4_0>(A, (b & 7) + 8 * (b >> 5), (b >> 3) & 3, smem);
     else wo_run(P, A.ogran, A.ocount, (unsigned) nattn * A.epoch, A.epoch, b - nattn, smem, A.err);
 }
+#endif
 
 int n_cus() {
     static int n = 0;
@@ -552,11 +554,11 @@ AttnDArgs attn_args(const AttnLaunch & A, void * gran, unsigned epoch) {
     a.exp_mode = A.exp_computed;
     a.err = A.err;
     // short contexts skip the score exchange: every workgroup of a head scores all n_kv
-    // positions itself (tools/probe: cheaper than the cross-workgroup hand-off up to ~128)
+    // positions itself (tools/probe r03: 4.8 vs 5.4 us at n_kv 33, 5.9 vs 6.3 at 101)
     static const int short_max = [] {
         const char * e = getenv("LVK_ATTN_SHORT");
         if (getenv("LVK_ATTN_NOEXCH") && atoi(getenv("LVK_ATTN_NOEXCH")) != 0) return 1 << 30;
-        return e ? atoi(e) : 64;
+        return e ? atoi(e) : 128;
     }();
     a.short_max = short_max;
     return a;
@@ -594,6 +596,7 @@ hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned e
     return hipGetLastError();
 }
 
+#ifdef LVK_DEV_KERNELS
 bool attention_wo_supported(int n_embd, int n_head, int n_ctx, const QMatrix & w) {
     if (!attention_decode_supported(n_embd, n_head, n_ctx)) return false;
     if (n_embd != wo::KT || w.qtype != Q4_0 || w.K != wo::KT || w.M <= 0 || w.M % 8) return false;
@@ -616,5 +619,11 @@ hipError_t launch_attention_wo(const AttnLaunch & A, const QMatrix & w, float * 
     LVK_LAUNCH(k_attn_wo, dim3(P.nwg + 4 * A.n_head), dim3(256), lds, s, a, P);
     return hipGetLastError();
 }
+#else
+bool attention_wo_supported(int, int, int, const QMatrix &) { return false; }
+hipError_t launch_attention_wo(const AttnLaunch &, const QMatrix &, float *, void *, unsigned, hipStream_t) {
+    return hipErrorNotSupported;
+}
+#endif
 
 }  // namespace lvk

@@ -44,6 +44,7 @@
 #include "lvk_kernels.h"
 #include "matvec_common.h"
 
+#ifdef LVK_DEV_KERNELS   // parked: built only into lib/dev (make -C llama.vk_amd dev)
 namespace lvk {
 
 namespace {
@@ -1052,3 +1053,18 @@ hipError_t launch_decode_persistent(const DecodeArgs & A, const DecodeArgs * A_d
 }
 
 }  // namespace lvk
+extern "C" __attribute__((visibility("default"))) int lvk_dev_kernels(void) { return 1; }
+#else
+extern "C" __attribute__((visibility("default"))) int lvk_dev_kernels(void) { return 0; }
+namespace lvk {
+// the product library does not carry the parked persistent kernel: a context never
+// selects it (lvk_set_decode_persistent keeps the launch-per-phase graph)
+bool decode_persistent_supported(int, int, int, int, int, int) { return false; }
+size_t decode_persistent_scratch_bytes(int, int) { return 16; }
+size_t decode_persistent_aq_d_floats(int, int) { return 0; }
+bool decode_persistent_prepare(DecodeArgs &, void *, int) { return false; }
+hipError_t launch_decode_persistent(const DecodeArgs &, const DecodeArgs *, int, hipStream_t) {
+    return hipErrorNotSupported;
+}
+}  // namespace lvk
+#endif

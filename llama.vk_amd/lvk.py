@@ -123,6 +123,7 @@ _sig("lvk_stage_layers", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c
 _sig("lvk_rccl_unique_id", C.c_int, [C.c_void_p, C.c_size_t])
 _sig("lvk_stage_connect", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_connect_shm", C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.c_int])
+_sig("lvk_dev_kernels", C.c_int, [])
 _sig("lvk_stage_step", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int])
 _sig("lvk_init_split", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, i32p, C.c_char_p, C.c_int])
 _sig("lvk_split_info", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)])
@@ -509,6 +510,11 @@ def gen_model(path, n_embd=4096, n_head=32, n_layer=32, ftype=2, seed=1, n_vocab
         cmd += ["--vocab", vocab]
     subprocess.check_call(cmd, stderr=subprocess.DEVNULL)
     return path
+
+
+def dev_kernels():
+    """True when the loaded library is the dev build (parked kernels compiled in)"""
+    return bool(lib.lvk_dev_kernels())
 
 
 def rccl_unique_id():

@@ -131,6 +131,8 @@ def test_7b_shaped_fused_attention_wo_matches(lvk, oracle, model_dir, monkeypatc
     """The opt-in one-launch attention + Wo (k_attn_wo, LVK_FUSE_ATTN_WO=1) on LLaMA-7B
     layer shapes: decode logits bit-identical to the oracle across 40 positions."""
     from oracle_lib import gen_model
+    if not lvk.dev_kernels():
+        pytest.skip("parked kernel: run with LVK_LIB=llama.vk_amd/lib/dev/libllama_vk_amd.so")
     path = gen_model(os.path.join(model_dir, "w4096_l2.bin"), n_embd=4096, n_head=32, n_layer=2, ftype=2, seed=7)
     monkeypatch.setenv("LVK_FUSE_ATTN_WO", "1")
     m = lvk.Llama(path, n_ctx=512)

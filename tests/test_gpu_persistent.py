@@ -1,5 +1,5 @@
-"""The persistent single-token decode kernel (decode_persistent.hip, opt-in through
-lvk_set_decode_persistent) against the reference goldens and the CPU oracle, bit for
+"""The persistent single-token decode kernel (decode_persistent.hip, parked: only in the
+dev build lib/dev, opt-in through lvk_set_decode_persistent) against the reference goldens and the CPU oracle, bit for
 bit: tiny Q4_0 models (the reference build's golden logits), a 70-step decode across
 the f16-dot tail boundaries, LLaMA-7B layer shapes (n_embd 4096, 32 heads, n_ff 11008)
 and LLaMA-65B layer shapes (n_embd 8192, 64 heads, n_ff 22016)."""
@@ -19,6 +19,8 @@ def bits(a):
 @pytest.fixture(scope="module")
 def lvk(gpu_available):
     import lvk as m
+    if not m.dev_kernels():
+        pytest.skip("parked kernel: run with LVK_LIB=llama.vk_amd/lib/dev/libllama_vk_amd.so")
     return m
 
 

@@ -3,6 +3,7 @@
 // and compares with the pure weight-stream floor measured by bw_probe.
 // Build: make -C tools/probe ; run on the GPU box.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -297,8 +298,28 @@ int main(int argc, char ** argv) {
                 first_entry = std::min(first_entry, (double) e[0]); last_entry = std::max(last_entry, (double) e[0]);
                 for (int q = 0; q < 3; q++) if (e[58 + q]) { a[q] += e[58 + q] - e[0]; c[q]++; }
             }
-            printf("  inputs-landed %.0f  weights-issued %.0f  norm-synced %.0f  (entry spread %.0f cycles)\n",
-                   c[0] ? a[0] / c[0] : -1.0, c[1] ? a[1] / c[1] : -1.0, c[2] ? a[2] / c[2] : -1.0, last_entry - first_entry);
+            printf("  inputs-landed %.0f  weights-issued %.0f  norm-synced %.0f\n",
+                   c[0] ? a[0] / c[0] : -1.0, c[1] ? a[1] / c[1] : -1.0, c[2] ? a[2] / c[2] : -1.0);
+            // per workgroup: the last wave's end; grouped by blockIdx % 8 (the XCD under
+            // round-robin placement) and the spread over workgroups
+            double xe[8] = {0}; int xn[8] = {0};
+            std::vector<double> wg_end;
+            for (int b = 0; b < 256; b++) {
+                double mx = 0; bool any = false;
+                for (int w = 0; w < 16; w++) {
+                    unsigned long long * e = &h[(size_t) (b * 16 + w) * 64];
+                    if (!e[0] || !e[3]) continue;
+                    any = true; mx = std::max(mx, (double) (e[3] - e[0]));
+                }
+                if (!any) continue;
+                wg_end.push_back(mx); xe[b % 8] += mx; xn[b % 8]++;
+            }
+            std::sort(wg_end.begin(), wg_end.end());
+            if (!wg_end.empty())
+                printf("  workgroup end: min %.0f p10 %.0f median %.0f p90 %.0f max %.0f | by b%%8:", wg_end.front(),
+                       wg_end[wg_end.size() / 10], wg_end[wg_end.size() / 2], wg_end[wg_end.size() * 9 / 10], wg_end.back());
+            for (int x = 0; x < 8; x++) printf(" %.0f", xn[x] ? xe[x] / xn[x] : 0.0);
+            printf("\n");
         }
         printf("  (loader waves %d) staged-issued %.0f  first-publish %.0f  end %.0f\n", npw, pe[0] / std::max(1, npw), pe[1] / std::max(1, npw), pe[2] / std::max(1, npw));
         for (int c = 0; c < 26 && cn[c]; c++)
