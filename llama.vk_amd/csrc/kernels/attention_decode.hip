@@ -73,6 +73,47 @@ __device__ __forceinline__ float quad_reduce(const float s[8]) {
     return (t0 + t1) + (t2 + t3);
 }
 
+// softmax exp (exp_f16 semantics) for EM != 0 without a vector load on the common path:
+// only NaN arguments (the table covers them; softmax arguments are <= 0 otherwise) take the
+// uploaded table, behind a wave-uniform branch, so no vmcnt wait -- which would also wait
+// for the V DMA in flight -- sits in the loop
+template <int EM>
+__device__ __forceinline__ uint16_t exp_softmax(uint16_t hx, const uint16_t * __restrict__ tab, int mode) {
+    if constexpr (EM < 0) {
+        return exp_f16(hx, tab, mode);
+    } else if constexpr (EM == 0) {
+        return tab[hx];
+    } else {
+        const float x = f16_to_f32(hx);
+        uint16_t e = f32_to_f16(EM == 2 ? expf(x) : (float) exp((double) x));
+        const bool table = !(((hx & 0x8000u) || hx == 0) && (hx & 0x7fffu) <= 0x7c00u);
+        if (__builtin_amdgcn_ballot_w64(table) != 0) {
+            const uint16_t t = tab[hx];
+            e = table ? t : e;
+            asm volatile("" : "+v"(e));
+        }
+        return e;
+    }
+}
+
+// fmaf(f16 half HA of a, f16 half HB of b, c): v_fma_mix converts both f16 operands
+// exactly and rounds once, the same result as fmaf on the converted values
+template <int HA, int HB>
+__device__ __forceinline__ float fma_mix_hh(uint32_t a, uint32_t b, float c) {
+    float d;
+    if constexpr (HA == 0 && HB == 0)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[1,1,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    else if constexpr (HA == 1 && HB == 1)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    else
+        static_assert(HA == HB, "same halves only");
+    return d;
+}
+
+// a workgroup barrier for LDS hand-offs only: __syncthreads() also drains vmcnt, which
+// would make every wave with V rows in flight wait for them
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 typedef unsigned long long u64g __attribute__((address_space(1)));
 typedef unsigned u32g __attribute__((address_space(1)));
 
@@ -100,11 +141,11 @@ __device__ __forceinline__ unsigned long long poll_granule(u64g * p, unsigned ep
 }
 
 #ifdef LVK_PROBE_TIMING   // dev probe builds only: per-wave s_memtime phase stamps
-__device__ unsigned long long g_dtrace[32 * 4 * 4 * 8];
-#define LVK_DT(ev)                                                                                       \
-    do {                                                                                                 \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                      \
-        if ((threadIdx.x & 63) == 0 && h < 32) g_dtrace[((h * 4 + sl) * 4 + (threadIdx.x >> 6)) * 8 + (ev)] = t_; \
+__device__ unsigned long long g_dtrace[32 * 4 * 4 * 16];
+#define LVK_DT(ev)                                                                                        \
+    do {                                                                                                  \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                       \
+        if ((threadIdx.x & 63) == 0 && h < 32) g_dtrace[((h * 4 + sl) * 4 + (threadIdx.x >> 6)) * 16 + (ev)] = t_; \
     } while (0)
 #else
 #define LVK_DT(ev) do { } while (0)
@@ -129,20 +170,27 @@ struct AttnDArgs {
     int short_max;                // n_kv <= short_max: no score exchange (every workgroup scores all)
 };
 
-// EXCH: the 4 workgroups of a head split the scores and exchange them as granules;
-// !EXCH: every workgroup scores all positions itself (4x the K reads, from the XCD's L2).
-// DYN: the choice is made per launch from n_kv (exchange only above A.short_max).
-template <int QT, bool EXCH = true, bool DYN = false>
+// The 4 workgroups of a head either split the scores and exchange them as granules, or
+// (n_kv <= A.short_max, DYN) every workgroup scores all positions itself (4x the K reads,
+// from the XCD's L2).  !DYN: always the exchange.  EM: the exp mode compiled in (exp_f16;
+// -1 reads A.exp_mode) -- a runtime mode puts the table path's load, and its vmcnt wait,
+// into the softmax loop.
+template <int QT, int EM, bool DYN = true>
 __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, const int sl, uint8_t * smem) {
     const int E = A.E, n_ctx = A.n_ctx, d0 = h * HD + sl * 32;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = tid & 3;
-    uint16_t * vl = (uint16_t *) smem;                           // [32 dims][n_ctx]
-    float * sc = (float *) (smem + (size_t) 32 * n_ctx * 2);     // [n_ctx]
+    const int VS = n_ctx + 32;                                   // V row stride (halves): rows 16 banks apart
+    uint16_t * vl = (uint16_t *) smem;                           // [32 dims][VS]
+    float * sc = (float *) (smem + (size_t) 32 * VS * 2);        // [n_ctx]
     uint16_t * pl = (uint16_t *) (sc + n_ctx);                   // [n_ctx]
     float * red = (float *) (pl + n_ctx);                        // 8 floats
     double * redd = (double *) (red + 8);                        // 4 doubles
     u64g * g = (u64g * ) (A.gran + (size_t) h * n_ctx);
     LVK_DT(0);
+    // the step block through the scalar cache (constant address space: s_load, counted by
+    // lgkmcnt): a vector load here would retire behind every Q / K / V load issued below
+    // (vmcnt is in order) and hold the n_kv-dependent loads back by a full HBM latency
+    const int n_past = ((const __attribute__((address_space(4))) StepParams *) A.sp)->n_past;
 
     // 1a. Loads that do not depend on n_past go out before the step block is read: Q,
     // the K rows of positions 0..63 (chunk 0; rows past n_kv are read, never used) and the
@@ -152,12 +200,15 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     uint4 qv[4];
 #pragma unroll
     for (int st = 0; st < 4; ++st) qv[st] = qp[st * 4];
-    auto v_dma = [&](int p0, int lo, int lim) {     // positions [max(p0, lo), min(p0 + 512, lim)) of the 32 rows
-        for (int row = wave; row < 32; row += 4)
+    auto v_dma = [&](int p0, int lo, int lim) {     // positions [max(p0, lo), min(p0 + 512, lim)) of rows 8 wave ..
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {               // a static count: the score waits can count past it
+            const int row = wave * 8 + i;
             if (p0 + lane * 8 >= lo && p0 + lane * 8 < lim)
                 __builtin_amdgcn_global_load_lds((const void *) (A.vc + (size_t) (d0 + row) * n_ctx + p0 + lane * 8),
-                                                 (__attribute__((address_space(3))) void *) (vl + (size_t) row * n_ctx + p0),
+                                                 (__attribute__((address_space(3))) void *) (vl + (size_t) row * VS + p0),
                                                  16, 0, 0);
+        }
     };
     uint4 kv[2][4];
     {
@@ -167,27 +218,28 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
         for (int st = 0; st < 4; ++st) kv[0][st] = kp[st * 4];
     }
     v_dma(0, 0, 64);
-    const int n_kv = A.sp->n_past + 1;
+    const int n_kv = n_past + 1;
     const int n_pad = (n_kv + 31) & ~31;
     const int np = n_kv & ~31;
-    const bool exch = DYN ? n_kv > A.short_max : EXCH;
-    // the rest of this workgroup's first two K chunks
+    const bool exch = DYN ? n_kv > A.short_max : true;
+    // the rest of this workgroup's first two K chunks; chunk 0 of an exchange is positions
+    // sl*64.. and lands in registers of its own (a reload into kv[0] would have to wait for
+    // the speculative load first)
+    const bool c0_other = exch && sl > 0;
+    uint4 kx[4];
+    if (c0_other) {
+        const int p = min(sl * 64 + (tid >> 2), n_kv - 1);
+        const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) kx[st] = kp[st * 4];
+    }
     {
-        const bool c0_other = exch && sl > 0;                    // chunk 0 of an exchange is position sl*64+
+        const int p = min((exch ? sl * 64 + 256 : 64) + (tid >> 2), n_kv - 1);
+        const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            if (c == 0 && !c0_other) continue;
-            const int base = exch ? sl * 64 + c * 256 : c * 64;
-            const int p = min(base + (tid >> 2), n_kv - 1);
-            const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
-#pragma unroll
-            for (int st = 0; st < 4; ++st) kv[c][st] = kp[st * 4];
-        }
+        for (int st = 0; st < 4; ++st) kv[1][st] = kp[st * 4];
     }
     LVK_DT(6);
-    for (int p0 = 0; p0 < n_pad; p0 += 512) v_dma(p0, 64, n_pad);
-    LVK_DT(7);
-    LVK_DT(1);
 
     // 1b. scores of chunks sl, sl+4, ... (exchange) or of every chunk (one position per lane quad)
     {
@@ -216,9 +268,14 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
         };
         const int cs = exch ? 256 : 64;                     // position stride of this workgroup's chunks
         const int cb = exch ? sl * 64 : 0;
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-            if (cb + c * cs < n_kv) score(kv[c], cb + c * cs + (tid >> 2));
+        if (c0_other) score(kx, cb + (tid >> 2));
+        else score(kv[0], cb + (tid >> 2));          // cb < n_kv: sl * 64 < n_kv when c0_other
+        if (cb + cs < n_kv) score(kv[1], cb + cs + (tid >> 2));
+        // the rest of the V slice goes out behind the first two chunks' scores: those wait
+        // only for their own K rows, the V rows are needed after the softmax
+        for (int p0 = 0; p0 < n_pad; p0 += 512) v_dma(p0, 64, n_pad);
+        LVK_DT(7);
+        LVK_DT(1);
         for (int c0 = cb + 2 * cs; c0 < n_kv; c0 += cs) {
             const int p = c0 + (tid >> 2);
             const uint4 * kp = (const uint4 *) (A.kc + (size_t) min(p, n_kv - 1) * E + h * HD) + r;
@@ -229,32 +286,50 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
         }
     }
     LVK_DT(2);
-    // 2. every score of the head: poll each granule until it carries this layer's epoch
+    // 2. softmax (ggml.c:7099-7121; no position is masked in a decode step).  Exchange: the
+    // granules are read four at a time; the ones without this layer's epoch are polled.
     float mx = -INFINITY;
-    if (!exch) __syncthreads();
-    for (int p = tid; p < n_kv; p += 256) {
-        const float v = exch ? __uint_as_float((unsigned) poll_granule(g + p, A.epoch, A.err)) : sc[p];
-        sc[p] = v;
-        mx = v > mx ? v : mx;
+    if (!exch) {
+        lds_barrier();
+        for (int p = tid; p < n_kv; p += 256) mx = sc[p] > mx ? sc[p] : mx;
+    } else {
+        for (int p0 = tid; p0 < n_kv; p0 += 1024) {
+            unsigned long long x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                x[k] = __hip_atomic_load(g + min(p0 + 256 * k, n_kv - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int p = p0 + 256 * k;
+                if (p < n_kv) {
+                    const unsigned long long y =
+                        (unsigned) (x[k] >> 32) == A.epoch ? x[k] : poll_granule(g + p, A.epoch, A.err);
+                    const float v = __uint_as_float((unsigned) y);
+                    sc[p] = v;
+                    mx = v > mx ? v : mx;
+                }
+            }
+        }
     }
     LVK_DT(3);
     mx = wave_max_f(mx);
     if (lane == 0) red[wave] = mx;
-    __syncthreads();
+    lds_barrier();
+    LVK_DT(8);
     {
         const float a = red[0] > red[1] ? red[0] : red[1], b = red[2] > red[3] ? red[2] : red[3];
         mx = a > b ? a : b;
     }
-    // softmax (ggml.c:7099-7121): no position is masked in a decode step
     double sum = 0.0;    // exact in any order: every term is an fp16 value in [0,1]
     for (int p = tid; p < n_kv; p += 256) {
-        const float e = f16_to_f32(exp_f16(f32_to_f16(sc[p] - mx), A.exp_tab, A.exp_mode));
+        const float e = f16_to_f32(exp_softmax<EM>(f32_to_f16(sc[p] - mx), A.exp_tab, A.exp_mode));
         sum += (double) e;
         sc[p] = e;
     }
     sum = wave_sum_d(sum);
     if (lane == 0) redd[wave] = sum;
-    __syncthreads();
+    lds_barrier();
+    LVK_DT(9);
     sum = (redd[0] + redd[1]) + (redd[2] + redd[3]);
     const float scl = (float) (1.0 / sum);
     for (int p = tid; p < n_pad; p += 256) pl[p] = p < n_kv ? f32_to_f16(sc[p] * scl) : (uint16_t) 0;
@@ -262,15 +337,15 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     __syncthreads();          // vmcnt(0) + barrier: the V DMA has landed too
     LVK_DT(5);
 
-    // P.V: quad q = dim d0 + q (waves 0-1)
+#ifdef LVK_ATTN_PV_QUAD   // probe A/B only: the round-2 P.V (a lane quad per dim on waves 0-1)
     float o = 0.0f;
+    const int q = tid >> 2;
+    const uint16_t * vr = vl + (size_t) q * VS;
     if (tid < 128) {
-        const int q = tid >> 2;
-        const uint16_t * vr = vl + (size_t) q * n_ctx;
         float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const int ns = np / 32;
         int st = 0;
-        for (; st + 2 <= ns; st += 2) {          // two steps' LDS reads in flight
+        for (; st + 2 <= ns; st += 2) {
             const uint4 v0 = *((const uint4 *) (vr + st * 32) + r), p0 = *((const uint4 *) (pl + st * 32) + r);
             const uint4 v1 = *((const uint4 *) (vr + st * 32 + 32) + r), p1 = *((const uint4 *) (pl + st * 32 + 32) + r);
             float vf[8], pf[8];
@@ -292,7 +367,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
         }
         const float res = quad_reduce(s);
         o = res;
-        if (np < n_kv) {      // leftovers in double, in position order (ggml.c:1806-1808)
+        if (np < n_kv) {
             double sumf = (double) res;
             for (int p = np; p < n_kv; ++p) {
                 const float prod = f16_to_f32(vr[p]) * f16_to_f32(pl[p]);
@@ -301,10 +376,85 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
             o = (float) sumf;
         }
     }
-    __syncthreads();
-    float * ob = sc;          // reuse: 32 outputs
-    if (tid < 128 && r == 0) ob[tid >> 2] = o;
-    __syncthreads();
+#define LVK_OB_LANE (tid < 128 && r == 0)
+#else
+    // P.V (ggml_vec_dot_f16, ggml.c:1781-1815): 8 threads per dim (wave w: dims 8w..8w+7),
+    // thread (r, hf) runs the AVX accumulators 4hf..4hf+3 of lane quad member r -- positions
+    // 32 st + 8 r + 4 hf + i -- with v_fma_mix (the f16 operands converted exactly, one
+    // rounding: fmaf of the converted values), then the F32Cx8 reduce order of quad_reduce.
+    float o = 0.0f;
+    const int q = tid >> 3, hf = (tid >> 2) & 1;
+    const uint16_t * vr = vl + (size_t) q * VS;
+    {
+        float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+        const int ns = np / 32;
+        const int off = r * 8 + hf * 4;
+        auto step = [&](int st) __attribute__((always_inline)) {
+            const uint2 v = *(const uint2 *) (vr + st * 32 + off);
+            const uint2 pp = *(const uint2 *) (pl + st * 32 + off);
+            s0 = fma_mix_hh<0, 0>(v.x, pp.x, s0);
+            s1 = fma_mix_hh<1, 1>(v.x, pp.x, s1);
+            s2 = fma_mix_hh<0, 0>(v.y, pp.y, s2);
+            s3 = fma_mix_hh<1, 1>(v.y, pp.y, s3);
+        };
+        int st = 0;
+        for (; st + 4 <= ns; st += 4) { step(st); step(st + 1); step(st + 2); step(st + 3); }
+        for (; st < ns; ++st) step(st);
+        // S[l] = (r0 + r1) + (r2 + r3) over the quad, then t_i = S[i] + S[i + 4] (halves 0, 1)
+        auto qsum = [](float v) {
+            const float v0 = quad_bcast<0>(v), v1 = quad_bcast<1>(v), v2 = quad_bcast<2>(v), v3 = quad_bcast<3>(v);
+            return (v0 + v1) + (v2 + v3);
+        };
+        // the other half's S (lane ^ 4 inside the 8-lane group): row_ror:n hands lane l the
+        // value of lane (l - n) mod 16, so half 0 takes ror 12 (l + 4), half 1 ror 4 (l - 4)
+        auto other = [&](float v) {
+            const int i = __builtin_bit_cast(int, v);
+            const int a = __builtin_amdgcn_update_dpp(0, i, 0x124, 0xF, 0xF, false);   // row_ror:4
+            const int b = __builtin_amdgcn_update_dpp(0, i, 0x12C, 0xF, 0xF, false);   // row_ror:12
+            return __builtin_bit_cast(float, hf ? a : b);
+        };
+        const float S0 = qsum(s0), S1 = qsum(s1), S2 = qsum(s2), S3 = qsum(s3);
+        const float t0 = S0 + other(S0), t1 = S1 + other(S1);
+        const float t2 = S2 + other(S2), t3 = S3 + other(S3);
+        o = (t0 + t1) + (t2 + t3);
+    }
+    if (np < n_kv) {
+        // leftovers in double, in position order (ggml.c:1806-1808): the 8 lanes of a dim form
+        // the products of positions np + 8k + lane (-0.0 past n_kv: an exact no-op in the sum),
+        // row_shl moves them to the dim's first lane, which adds them in order
+        const int sub = tid & 7;
+        float pr[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int p = np + 8 * k + sub;
+            pr[k] = p < n_kv ? f16_to_f32(vr[p]) * f16_to_f32(pl[p]) : -0.0f;
+        }
+        double sumf = (double) o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (8 * k >= n_kv - np) break;
+            const int i = __builtin_bit_cast(int, pr[k]);
+            float v[8];
+            v[0] = pr[k];
+            v[1] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x101, 0xF, 0xF, false));
+            v[2] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x102, 0xF, 0xF, false));
+            v[3] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x103, 0xF, 0xF, false));
+            v[4] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x104, 0xF, 0xF, false));
+            v[5] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x105, 0xF, 0xF, false));
+            v[6] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x106, 0xF, 0xF, false));
+            v[7] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x107, 0xF, 0xF, false));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sumf += (double) v[j];
+        }
+        o = (float) sumf;     // meaningful in the dim's first lane
+    }
+#define LVK_OB_LANE ((tid & 7) == 0)
+#endif
+    LVK_DT(10);
+    float * ob = sc;          // reuse: 32 outputs (sc was last read before the barrier above)
+    if (LVK_OB_LANE) ob[q] = o;
+#undef LVK_OB_LANE
+    lds_barrier();
     if (tid < 32) {
         const float v = ob[tid];
         if (A.out_f32) A.out_f32[d0 + tid] = v;
@@ -353,12 +503,13 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
             }
         }
     }
+    LVK_DT(11);
 }
 
-template <int QT, bool EXCH>
+template <int QT, int EM>
 __global__ __launch_bounds__(256) void k_attn_d(AttnDArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    attn_d_run<QT, EXCH, true>(A, blockIdx.x, blockIdx.y, smem);
+    attn_d_run<QT, EM>(A, blockIdx.x, blockIdx.y, smem);
 }
 
 #ifdef LVK_DEV_KERNELS   // parked (measured slower than two launches): lib/dev only
@@ -516,24 +667,16 @@ __global__ __launch_bounds__(256) void k_attn_wo(AttnDArgs A, WoArgs P) {
     // attention workgroups first (dispatched first, one per CU on half the chip; the 4
     // slices of a head on one XCD as in k_attn_d's (H, 4) grid), then the Wo workgroups
     const int nattn = (int) gridDim.x - P.nwg;
-    if (b < nattn) attn_d_run<Q4_0>(A, (b & 7) + 8 * (b >> 5), (b >> 3) & 3, smem);
+    if (b < nattn) attn_d_run<Q4_0, -1, false>(A, (b & 7) + 8 * (b >> 5), (b >> 3) & 3, smem);
     else wo_run(P, A.ogran, A.ocount, (unsigned) nattn * A.epoch, A.epoch, b - nattn, smem, A.err);
 }
 #endif
 
-int n_cus() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0, v = 0;
-        n = (hipGetDevice(&dev) == hipSuccess &&
-             hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-                ? v
-                : 256;
-    }
-    return n;
-}
+#ifdef LVK_DEV_KERNELS
+int n_cus() { return cu_count(); }
+#endif
 
-size_t attn_lds(int n_ctx) { return (size_t) 32 * n_ctx * 2 + (size_t) n_ctx * 6 + 64; }
+size_t attn_lds(int n_ctx) { return (size_t) 32 * (n_ctx + 32) * 2 + (size_t) n_ctx * 6 + 64; }
 
 AttnDArgs attn_args(const AttnLaunch & A, void * gran, unsigned epoch) {
     AttnDArgs a{};
@@ -585,14 +728,16 @@ hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned e
     if (A.out_qtype != Q4_0 && A.out_qtype != Q4_1) return hipErrorNotSupported;
     const AttnDArgs a = attn_args(A, gran, epoch);
     const size_t lds = attn_lds(A.n_ctx);
-    static const bool exch = !(getenv("LVK_ATTN_NOEXCH") && atoi(getenv("LVK_ATTN_NOEXCH")) != 0);
-    if (A.out_qtype == Q4_1) {
-        if (exch) LVK_LAUNCH((k_attn_d<Q4_1, true>), dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
-        else LVK_LAUNCH((k_attn_d<Q4_1, false>), dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
-    } else {
-        if (exch) LVK_LAUNCH((k_attn_d<Q4_0, true>), dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
-        else LVK_LAUNCH((k_attn_d<Q4_0, false>), dim3(A.n_head, HD / 32), dim3(256), lds, s, a);
+    const dim3 grid(A.n_head, HD / 32);
+#define LVK_ATTN_EM(QT_)                                                                      \
+    switch (a.exp_mode) {                                                                     \
+        case 2: LVK_LAUNCH((k_attn_d<QT_, 2>), grid, dim3(256), lds, s, a); break;            \
+        case 1: LVK_LAUNCH((k_attn_d<QT_, 1>), grid, dim3(256), lds, s, a); break;            \
+        default: LVK_LAUNCH((k_attn_d<QT_, 0>), grid, dim3(256), lds, s, a); break;           \
     }
+    if (A.out_qtype == Q4_1) { LVK_ATTN_EM(Q4_1) }
+    else { LVK_ATTN_EM(Q4_0) }
+#undef LVK_ATTN_EM
     return hipGetLastError();
 }
 

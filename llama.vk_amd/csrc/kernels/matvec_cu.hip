@@ -489,16 +489,19 @@ hipError_t go(const CuParams & P, hipStream_t s) {
 
 }  // namespace
 
+// CUs of the current device, cached per device id (a one-process layer split may drive
+// devices of different sizes or CU-masked partitions)
 int cu_count() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess) return 256;
-        hipDeviceProp_t p;
-        if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 256;
-        n = p.multiProcessorCount;
+    constexpr int MAXDEV = 64;
+    static int n[MAXDEV] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (dev < 0 || dev >= MAXDEV) dev = 0;
+    if (n[dev] == 0) {
+        int v = 0;
+        n[dev] = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
     }
-    return n;
+    return n[dev];
 }
 
 #ifdef LVK_PROBE_TIMING

@@ -1,7 +1,7 @@
 """Failure paths of the device-side waits (no silent wrong answers).
 
 The decode attention's workgroups wait on each other's score granules with a
-bounded spin.  The probe build (make -C llama.vk_amd probe) never publishes
+bounded spin (with LVK_ATTN_SHORT=0 at every n_kv; by default only past 128).  The probe build (make -C llama.vk_amd probe) never publishes
 position 0's score and gives up after 4096 polls: the timeout must reach the
 host as a failed llama_eval (rc 1) / lvk_eval_greedy (-1) and invalid logits,
 and the context must stay usable.  Runs in a child process, because lvk.py
@@ -46,7 +46,7 @@ m.close()
 def test_attention_wait_timeout_fails_the_eval(tiny_models, gpu_available):
     if not os.path.exists(PROBE):
         pytest.fail("probe library not built (make -C llama.vk_amd probe)")
-    env = dict(os.environ, LVK_LIB=PROBE)
+    env = dict(os.environ, LVK_LIB=PROBE, LVK_ATTN_SHORT="0")   # every decode step exchanges scores
     code = CHILD % {"pkg": os.path.join(ROOT, "llama.vk_amd"), "model": tiny_models["tiny_q4_0"]}
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     out = r.stdout

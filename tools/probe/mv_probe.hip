@@ -215,7 +215,7 @@ int main(int argc, char ** argv) {
         const int kind = getenv("LVK_TRACE_KIND") ? atoi(getenv("LVK_TRACE_KIND")) : 5;
         if (kind == 1 && !getenv("LVK_ATTN_V1")) {
             void * at = lvk_probe_dtrace();
-            std::vector<unsigned long long> h(32 * 4 * 4 * 8);
+            std::vector<unsigned long long> h(32 * 4 * 4 * 16);
             for (int l = 0; l < 4; l++) op(1, l);
             CK(hipStreamSynchronize(s));
             CK(hipMemset(gran, 0, attention_decode_scratch_bytes(H, C)));
@@ -223,20 +223,22 @@ int main(int argc, char ** argv) {
             op(1, 4);
             CK(hipStreamSynchronize(s));
             CK(hipMemcpy(h.data(), at, h.size() * 8, hipMemcpyDeviceToHost));
-            double acc[8] = {0}; int n = 0;
-            unsigned long long t0min = ~0ull;
-            for (int w = 0; w < 32 * 4 * 4; w++) if (h[w * 8]) t0min = std::min(t0min, h[w * 8]);
-            double start_sp = 0;
+            // per wave: cycles from its entry; per workgroup: entry spread and last end
+            double acc[16] = {0}, mxv[16] = {0}; int n = 0;
+            unsigned long long t0min = ~0ull, t0max = 0, tend = 0;
             for (int w = 0; w < 32 * 4 * 4; w++) {
-                unsigned long long * e = &h[(size_t) w * 8];
-                if (!e[0] || !e[5]) continue;
+                unsigned long long * e = &h[(size_t) w * 16];
+                if (!e[0] || !e[11]) continue;
                 n++;
-                start_sp += (double) (e[0] - t0min);
-                for (int k = 1; k < 7; k++) acc[k] += (double) (e[k] - e[0]);
+                t0min = std::min(t0min, e[0]); t0max = std::max(t0max, e[0]); tend = std::max(tend, e[11]);
+                for (int k = 1; k < 12; k++) { acc[k] += (double) (e[k] - e[0]); mxv[k] = std::max(mxv[k], (double) (e[k] - e[0])); }
             }
-            double a7 = 0; for (int w = 0; w < 32 * 4 * 4; w++) { unsigned long long * e = &h[(size_t) w * 8]; if (e[0] && e[5]) a7 += (double) (e[7] - e[0]); }
-            printf("decode attention trace (%d waves): qk-issued %.0f  v0-dma %.0f  sp+dma-issued %.0f  scores %.0f  exchange %.0f  softmax %.0f  dma-wait %.0f cycles\n",
-                   n, acc[6] / n, a7 / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+            const char * nm[12] = {"", "dma-issued", "scores", "exchange", "softmax", "dma-wait", "qk-issued", "v-dma", "max-sync", "sum-sync", "pv", "end"};
+            const int ord[11] = {6, 7, 1, 2, 3, 8, 9, 4, 5, 10, 11};
+            printf("decode attention trace (%d waves, entry spread %llu, first entry -> last end %llu cycles), avg (max) from wave entry:\n ",
+                   n, t0max - t0min, tend - t0min);
+            for (int i = 0; i < 11; i++) printf(" %s %.0f (%.0f)", nm[ord[i]], acc[ord[i]] / n, mxv[ord[i]]);
+            printf("\n");
             return 0;
         }
         if (kind == 1) {
