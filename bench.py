@@ -509,16 +509,39 @@ def run(args, coord):
         m.eval(ptoks, 0)
         tok = int(np.argmax(m.logits()[-1]))
         tok_first = tok
+        seq_g = []
         coord.barrier()
         t0 = time.perf_counter()
         for i in range(args.steps):
             tok = m.eval_greedy(tok, 16 + (i % (n_ctx - 16)))
+            seq_g.append(tok)
         t1 = time.perf_counter()
         coord.barrier()
         el_g = coord.max(t1 - t0)
         greedy = {"value": n_gpus * args.steps / el_g, "unit": "tok/s", "ms_per_step": el_g / args.steps * 1e3,
                   "path": "lvk_eval_greedy: decode graph ending in the device argmax, 4-byte D2H",
                   "first_token": tok_first}
+        # the same greedy steps chained on the device (lvk_decode_greedy): one call per pass
+        # over positions 16..n_ctx-1, the step graph replayed back to back; its tokens must be
+        # the per-step loop's
+        m.eval(ptoks, 0)
+        seq_c = []
+        coord.barrier()
+        t0 = time.perf_counter()
+        tok, i = tok_first, 0
+        while i < args.steps:
+            pos = 16 + (i % (n_ctx - 16))
+            n = min(args.steps - i, n_ctx - pos)
+            part = m.decode_greedy(tok, pos, n)
+            seq_c.extend(int(t) for t in part)
+            tok, i = int(part[-1]), i + n
+        t1 = time.perf_counter()
+        coord.barrier()
+        el_c = coord.max(t1 - t0)
+        greedy["chained"] = {"value": n_gpus * args.steps / el_c, "unit": "tok/s", "ms_per_step": el_c / args.steps * 1e3,
+                             "path": "lvk_decode_greedy: one call per pass over positions 16..511, the step graph "
+                                     "replayed back to back (argmax, step block and next embedding row on the device)",
+                             "tokens_match_eval_greedy": seq_c == seq_g}
         # host sampler (llama_sample_top_p_top_k, main's defaults: top_k 40, top_p 0.95, temp 0.8,
         # repeat_penalty 1.1 over a 64-token window) on fresh logits (lvk_eval_greedy leaves none)
         m.eval([tok], 16)

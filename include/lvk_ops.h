@@ -119,6 +119,14 @@ LVK_API int lvk_decode_persistent_active(struct llama_context * ctx);
  * lvk_argmax(x, n) is the op-level kernel on a host array: the first index whose
  * value is strictly greater than all earlier ones (0 when x[0] is NaN). */
 LVK_API int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past);
+/* n_steps greedy decode steps in one call: out_tokens[i] is what the i-th of the calls
+ * t = lvk_eval_greedy(ctx, t, n_past + i) (t starting at `token`) would return, and the KV
+ * cache ends in the same state.  The steps run as back-to-back replays of one decode graph
+ * whose last kernel advances the step block and writes the next embedding row on the device,
+ * so nothing crosses PCIe between steps.  n_past + n_steps <= n_ctx.  Returns 0, or -1 on
+ * error (layer splits, logits_all contexts and the opt-in persistent kernel refuse it).
+ * The host logits of llama_get_logits are NOT refreshed. */
+LVK_API int lvk_decode_greedy(struct llama_context * ctx, int token, int n_past, int n_steps, int * out_tokens);
 /* On-device sampling: lvk_eval_sample(ctx, token, n_past, last_n, n_last,
  * top_k, top_p, temp, repeat_penalty) returns what llama_eval(ctx, &token, 1, n_past, .)
  * followed by llama_sample_top_p_top_k(ctx, last_n, n_last, top_k, top_p, temp,

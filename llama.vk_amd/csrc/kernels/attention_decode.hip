@@ -168,6 +168,7 @@ struct AttnDArgs {
     int exp_mode;
     unsigned * err;               // host-mapped error word (nullptr: none)
     int short_max;                // n_kv <= short_max: no score exchange (every workgroup scores all)
+    int seq_epochs;               // epoch += sp->seq << 7 (granules never zeroed between tokens)
 };
 
 // The 4 workgroups of a head either split the scores and exchange them as granules, or
@@ -190,7 +191,10 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     // the step block through the scalar cache (constant address space: s_load, counted by
     // lgkmcnt): a vector load here would retire behind every Q / K / V load issued below
     // (vmcnt is in order) and hold the n_kv-dependent loads back by a full HBM latency
-    const int n_past = ((const __attribute__((address_space(4))) StepParams *) A.sp)->n_past;
+    const __attribute__((address_space(4))) StepParams * spc = (const __attribute__((address_space(4))) StepParams *) A.sp;
+    const int n_past = spc->n_past;
+    // this layer's granule tag: unique per (step, layer) when the step counter is used
+    const unsigned ep = A.seq_epochs ? A.epoch + (spc->seq << 7) : A.epoch;
 
     // 1a. Loads that do not depend on n_past go out before the step block is read: Q,
     // the K rows of positions 0..63 (chunk 0; rows past n_kv are read, never used) and the
@@ -262,7 +266,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
 #ifdef LVK_PROBE_DROP_GRANULE   // fault-injection probe build only: position 0's score is never published
                 else if (p == 0) {}
 #endif
-                else __hip_atomic_store(g + p, ((unsigned long long) A.epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                else __hip_atomic_store(g + p, ((unsigned long long) ep << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
         };
@@ -303,7 +307,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
                 const int p = p0 + 256 * k;
                 if (p < n_kv) {
                     const unsigned long long y =
-                        (unsigned) (x[k] >> 32) == A.epoch ? x[k] : poll_granule(g + p, A.epoch, A.err);
+                        (unsigned) (x[k] >> 32) == ep ? x[k] : poll_granule(g + p, ep, A.err);
                     const float v = __uint_as_float((unsigned) y);
                     sc[p] = v;
                     mx = v > mx ? v : mx;
@@ -704,6 +708,7 @@ AttnDArgs attn_args(const AttnLaunch & A, void * gran, unsigned epoch) {
         return e ? atoi(e) : 128;
     }();
     a.short_max = short_max;
+    a.seq_epochs = A.seq_epochs;
     return a;
 }
 
@@ -757,6 +762,7 @@ hipError_t launch_attention_wo(const AttnLaunch & A, const QMatrix & w, float * 
         A.out_qtype != Q4_0 || !y)
         return hipErrorNotSupported;
     AttnDArgs a = attn_args(A, gran, epoch);
+    a.seq_epochs = 0;     // its output counter needs the per-token zeroing anyway
     a.ogran = a.gran + (size_t) A.n_head * A.n_ctx;
     a.ocount = (unsigned *) (a.ogran + (size_t) A.n_head * (HD / 32) * 5);   // inside the 6-per-block room
     const WoArgs P{w.nib, (const float4 *) w.scl, w.M / 8, y, std::min(n_cus(), w.M / 8)};

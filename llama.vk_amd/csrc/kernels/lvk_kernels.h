@@ -76,12 +76,14 @@ struct ActQ {
 };
 
 // the runtime scalar block the decode graph reads (so one captured graph
-// serves every position): written by a 16-byte H2D copy before each step.
+// serves every position): written by a 16-byte H2D copy before each step, or advanced
+// on the device by k_argmax_step in a chained greedy decode.
 struct StepParams {
     int n_past;
     int n_tokens;
     int pad0;       // the token of a single-token eval (read by the embedding kernel)
-    int pad1;
+    unsigned seq;   // decode step counter: the decode attention's granule epochs are
+                    // (seq << 7) + layer + 1, so the granules need no zeroing per token
 };
 
 struct RopeTable {            // host-built with glibc powf/cosf/sinf (ggml.c:7209-7213)
@@ -152,6 +154,7 @@ struct AttnLaunch {
     int exp_computed = 0;     // exp mode (lvk_device.h exp_f16): 0 table, 1 double, 2 f32 -- nonzero only after exp_check
     unsigned * err = nullptr; // host-mapped error word (DevError); kernels that spin report a timeout here
     int kv32 = 0;             // f32 K, V and queries (f16_kv = false): launch_attention only
+    int seq_epochs = 0;       // decode attention: granule epoch = (sp->seq << 7) + epoch (no per-token zeroing)
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
 // prompt batches (N > 1, Q4_0 / Q4_1 output): scores+softmax per (head, 32 tokens) then
@@ -330,6 +333,11 @@ hipError_t launch_rmsnorm_rows(const float * x, const float * g, int K, int n, f
 // greedy argmax over x[0..n) with the reference's first-maximum rule (llama.cpp:1382-1394); *out on the device
 // (out2, optional: a second copy of the token, e.g. host-mapped memory)
 hipError_t launch_argmax(const float * x, int n, int * out, hipStream_t s, int * out2 = nullptr);
+// one chained greedy step's tail (lvk_decode_greedy): the same argmax, the token into
+// chain[1 + chain[0]++], the step block advanced (n_past + 1, token, seq + 1) and the token's
+// embedding row (launch_embed's) into x[0..n_embd)
+hipError_t launch_argmax_step(const float * logits, int n, StepParams * sp, int * chain, const void * emb, int emb_type,
+                              int n_embd, float * x, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // ggml graph operators (graph_ops.hip; include/ggml.h via runtime/ggml_graph.cpp): one

@@ -80,7 +80,7 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
-    int tq = 4;   // trace event index (probe builds)
+    [[maybe_unused]] int tq = 4;   // trace event index (probe builds)
     LVK_T(0);
 
     if (NP > 0 && wave >= NW) {

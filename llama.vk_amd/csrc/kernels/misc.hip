@@ -343,7 +343,77 @@ __global__ __launch_bounds__(1024) void k_argmax_first(const float * __restrict_
         if (out2) out2[0] = tok;     // e.g. host-mapped memory: visible after the stream completes
     }
 }
+
+// the last kernel of a chained greedy step (lvk_decode_greedy): the argmax of k_argmax_first
+// is the next token; it goes to chain[1 + i] (chain[0] counts the steps), into the step block
+// (n_past + 1, the token, seq + 1) and, as its embedding row (k_embed's dequantization), into
+// x -- everything the next replay of the step graph reads
+__global__ __launch_bounds__(1024) void k_argmax_step(const float * __restrict__ logits, int n, StepParams * sp,
+                                                      int * chain, const uint8_t * __restrict__ emb, int type, int E,
+                                                      float * __restrict__ x) {
+    __shared__ ArgBest red[16];
+    __shared__ int s_tok;
+    ArgBest b{-INFINITY, INT_MAX};
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const float v = logits[i];
+        if (v == v && (b.i == INT_MAX || v > b.v)) b = {v, i};
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        ArgBest o;
+        o.v = __shfl_xor(b.v, off, 64);
+        o.i = __shfl_xor(b.i, off, 64);
+        b = arg_pick(b, o);
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ArgBest r = red[0];
+        for (int w = 1; w < 16; ++w) r = arg_pick(r, red[w]);
+        const bool nan0 = n > 0 && !(logits[0] == logits[0]);
+        const int tok = (nan0 || r.i == INT_MAX) ? 0 : r.i;
+        s_tok = tok;
+        const int i = chain[0];
+        chain[1 + i] = tok;
+        chain[0] = i + 1;
+        StepParams st = *sp;
+        st.n_past += 1;
+        st.pad0 = tok;
+        st.seq += 1;
+        *sp = st;
+    }
+    __syncthreads();
+    const size_t tok = (size_t) s_tok;
+    for (int e = threadIdx.x; e < E; e += 1024) {
+        float v;
+        if (type == Q4_0) {
+            const uint8_t * blk = emb + tok * (size_t) (E / 32) * 20 + (size_t) (e / 32) * 20;
+            const float d = *(const float *) blk;
+            const uint8_t byte = blk[4 + (e % 32) / 2];
+            const int qv = (e & 1) ? (byte >> 4) : (byte & 15);
+            v = (float) (qv - 8) * d;
+        } else if (type == Q4_1) {
+            const uint8_t * blk = emb + tok * (size_t) (E / 32) * 24 + (size_t) (e / 32) * 24;
+            const float d = *(const float *) blk, m = *(const float *) (blk + 4);
+            const uint8_t byte = blk[8 + (e % 32) / 2];
+            const int qv = (e & 1) ? (byte >> 4) : (byte & 15);
+            const float a = (float) qv * d;
+            v = a + m;
+        } else if (type == 1) {
+            v = f16_to_f32(((const uint16_t *) emb)[tok * E + e]);
+        } else {
+            v = ((const float *) emb)[tok * E + e];
+        }
+        x[e] = v;
+    }
+}
 }  // namespace
+
+hipError_t launch_argmax_step(const float * logits, int n, StepParams * sp, int * chain, const void * emb, int emb_type,
+                              int n_embd, float * x, hipStream_t s) {
+    if (n <= 0 || n_embd <= 0 || n_embd % 32) return hipErrorInvalidValue;
+    LVK_LAUNCH(k_argmax_step, dim3(1), dim3(1024), 0, s, logits, n, sp, chain, (const uint8_t *) emb, emb_type, n_embd, x);
+    return hipGetLastError();
+}
 
 hipError_t launch_argmax(const float * x, int n, int * out, hipStream_t s, int * out2) {
     if (n <= 0) return hipErrorInvalidValue;

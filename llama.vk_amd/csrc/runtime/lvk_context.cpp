@@ -66,6 +66,9 @@ Context::~Context() {
     if (graph_greedy) (void) hipGraphDestroy(graph_greedy);
     if (graph_sample_exec) (void) hipGraphExecDestroy(graph_sample_exec);
     if (graph_sample) (void) hipGraphDestroy(graph_sample);
+    if (graph_chain_exec) (void) hipGraphExecDestroy(graph_chain_exec);
+    if (graph_chain) (void) hipGraphDestroy(graph_chain);
+    if (chain_h) (void) hipHostFree(chain_h);
     if (samp_h) (void) hipHostFree(samp_h);
     if (sout_h) (void) hipHostFree(sout_h);
     if (greedy_h) (void) hipHostFree(greedy_h);
@@ -119,6 +122,9 @@ void Context::init(const llama_context_params & p) {
         old_attention = getenv("LVK_ATTN_V1") && atoi(getenv("LVK_ATTN_V1")) != 0;
         fuse_attn_wo = getenv("LVK_FUSE_ATTN_WO") && atoi(getenv("LVK_FUSE_ATTN_WO")) != 0;
         attn_gran = model.alloc(attention_decode_scratch_bytes((int) H, (int) C));
+        LVK_HIP(hipMemset(attn_gran, 0, attention_decode_scratch_bytes((int) H, (int) C)));
+        // granule tags (seq << 7) + layer + 1 stay unique per token with up to 126 layers
+        seq_epochs = !fuse_attn_wo && L <= 126;
     }
     {
         // persistent decode state: the layer table and the in-launch exchange buffers
@@ -161,6 +167,8 @@ void Context::init(const llama_context_params & p) {
     *err_h = 0;
     LVK_HIP(hipHostGetDevicePointer((void **) &err_d, err_h, 0));
     greedy_d = (int *) model.alloc(4);
+    chain_d = (int *) model.alloc((1 + C) * 4);
+    LVK_HIP(hipHostMalloc((void **) &chain_h, C * 4, hipHostMallocDefault));
     // the device argmax also stores the token straight into host-mapped memory
     LVK_HIP(hipHostMalloc((void **) &greedy_h, 64, hipHostMallocMapped | hipHostMallocCoherent));
     LVK_HIP(hipHostGetDevicePointer((void **) &greedy_hd, greedy_h, 0));
@@ -298,7 +306,7 @@ bool Context::use_mfma(int n) const {
     return true;
 }
 
-void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int logit_row, bool head) {
+void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int logit_row, bool head, bool embed) {
     const HParams & hp = model.hp;
     if (!tok_src) tok_src = tok_d;
     float * const logits_out = logits_d + (size_t) logit_row * hp.n_vocab;
@@ -381,10 +389,11 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
     // attention, Wo and the residual add in one launch (attention_decode.hip, k_attn_wo)
     const bool attn_wo = n == 1 && !old_attention && !kv32 && fuse_attn_wo && model.qtype == Q4_0 && !model.layers.empty() &&
                          attention_wo_supported(E, H, n_ctx, model.layers[0].wo);
-    if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx))
+    const bool seq_ep = seq_epochs && !attn_wo;
+    if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx) && !seq_ep)
         // the decode attention's score granules carry epoch = layer + 1: zero them once per token
         LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes(H, n_ctx), stream));
-    if (model.has_embed)
+    if (model.has_embed && embed)
         // a single-token eval takes its token from the step block (one H2D copy per token)
         timed_launch(K_EMBED, 0, [&] {
             return launch_embed(model.tok_emb, model.emb_type, E, n == 1 ? &sp_d->pad0 : tok_src, n, x, stream);
@@ -400,6 +409,7 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
         at.exp_computed = exp_computed;
         at.err = err_d;
         at.kv32 = kv32;
+        at.seq_epochs = seq_ep ? 1 : 0;
         if (attn_wo) {
             timed_launch(K_ATTN_WO, qbytes(ly.wo), [&] {
                 return launch_attention_wo(at, ly.wo, x, attn_gran, (unsigned) il + 1, stream);
@@ -447,24 +457,32 @@ void Context::build_graph(int kind) {
     // variant copies the sampler block in and ends in the device top-k candidates
     LVK_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
-        LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
-        if (kind == 2) LVK_HIP(hipMemcpyAsync(samp_d, samp_h, sizeof(SampleParams), hipMemcpyHostToDevice, stream));
-        enqueue_forward(1, true);
-        if (kind == 1) {
-            enqueue_argmax();
-        } else if (kind == 2) {
-            LVK_HIP(launch_sample_cand(logits_d, (int) model.hp.n_vocab, samp_d, sout_d, stream));
-        } else if (model.has_head) {
-            LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost,
-                                   stream));
+        if (kind == 3) {
+            // a chained step: the step block and x were left by the previous step (or the
+            // call's setup); the argmax advances both for the next replay
+            enqueue_forward(1, true, nullptr, 0, true, false);
+            LVK_HIP(launch_argmax_step(logits_d, (int) model.hp.n_vocab, sp_d, chain_d, model.tok_emb, model.emb_type,
+                                       (int) model.hp.n_embd, x, stream));
+        } else {
+            LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
+            if (kind == 2) LVK_HIP(hipMemcpyAsync(samp_d, samp_h, sizeof(SampleParams), hipMemcpyHostToDevice, stream));
+            enqueue_forward(1, true);
+            if (kind == 1) {
+                enqueue_argmax();
+            } else if (kind == 2) {
+                LVK_HIP(launch_sample_cand(logits_d, (int) model.hp.n_vocab, samp_d, sout_d, stream));
+            } else if (model.has_head) {
+                LVK_HIP(hipMemcpyAsync(logits.data(), logits_d, sizeof(float) * logits.size(), hipMemcpyDeviceToHost,
+                                       stream));
+            }
         }
     } catch (...) {
         hipGraph_t g;
         (void) hipStreamEndCapture(stream, &g);
         throw;
     }
-    hipGraph_t & g = kind == 1 ? graph_greedy : kind == 2 ? graph_sample : graph;
-    hipGraphExec_t & ge = kind == 1 ? graph_greedy_exec : kind == 2 ? graph_sample_exec : graph_exec;
+    hipGraph_t & g = kind == 1 ? graph_greedy : kind == 2 ? graph_sample : kind == 3 ? graph_chain : graph;
+    hipGraphExec_t & ge = kind == 1 ? graph_greedy_exec : kind == 2 ? graph_sample_exec : kind == 3 ? graph_chain_exec : graph_exec;
     LVK_HIP(hipStreamEndCapture(stream, &g));
     LVK_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
 }
@@ -486,6 +504,54 @@ int Context::eval_greedy(int token, int n_past) {
     begin_eval_safe(&token, 1, n_past, part);
     end_eval(true);
     return *greedy_h;
+}
+
+// the step counter of the next device step (StepParams::seq); before it would run past the
+// 25 bits that keep (seq << 7) + layer + 1 unique, the granules are zeroed (stream-ordered
+// ahead of the steps that use the restarted counter) and the count restarts
+unsigned Context::next_seq(unsigned k) {
+    if (seq + k >= (1u << 25)) {
+        if (attn_gran)
+            LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes((int) model.hp.n_head, n_ctx), stream));
+        seq = 0;
+    }
+    const unsigned first = seq + 1;
+    seq += k;
+    return first;
+}
+
+// n_steps greedy decode steps in one call (lvk_decode_greedy): the same tokens as n_steps
+// calls of eval_greedy(token_i, n_past + i) with token_{i+1} their result, but the host
+// only sets the step block up once and replays the chained graph back to back (no host
+// round trip, step-block copy or embedding launch between the steps).  out[0..n_steps).
+int Context::decode_greedy(int token, int n_past, int n_steps, int * out) {
+    if (!model.has_head || !model.has_embed) throw Error("llama.vk_amd: greedy decode needs the whole model");
+    if (logits_all) throw Error("llama.vk_amd: greedy decode needs last-token logits");
+    if (n_steps <= 0 || n_past < 0 || n_past + n_steps > n_ctx_user)
+        throw Error("llama.vk_amd: n_past + n_steps exceeds n_ctx");
+    if (token < 0 || token >= (int) model.hp.n_vocab) throw Error("llama.vk_amd: token id out of range");
+    if (!use_graph || profiling || persistent_ok())
+        throw Error("llama.vk_amd: greedy decode chains need the launch-per-phase decode graph");
+    try {
+        StepParams * sh = sp_h;
+        sh->n_past = n_past;
+        sh->n_tokens = 1;
+        sh->pad0 = token;
+        sh->seq = next_seq((unsigned) n_steps);     // the steps take seq, seq + 1, ...
+        LVK_HIP(hipMemcpyAsync(sp_d, sh, sizeof(StepParams), hipMemcpyHostToDevice, stream));
+        LVK_HIP(hipMemsetAsync(chain_d, 0, sizeof(int), stream));
+        LVK_HIP(launch_embed(model.tok_emb, model.emb_type, (int) model.hp.n_embd, &sp_d->pad0, 1, x, stream));
+        if (!graph_chain_exec) build_graph(3);
+        for (int i = 0; i < n_steps; ++i) LVK_HIP(hipGraphLaunch(graph_chain_exec, stream));
+        LVK_HIP(hipMemcpyAsync(chain_h, chain_d + 1, sizeof(int) * (size_t) n_steps, hipMemcpyDeviceToHost, stream));
+    } catch (...) {
+        (void) hipStreamSynchronize(stream);
+        logits_valid = false;
+        throw;
+    }
+    end_eval(true);
+    std::memcpy(out, chain_h, sizeof(int) * (size_t) n_steps);
+    return out[n_steps - 1];
 }
 
 // One decode step whose sampler runs its O(n_vocab) part on the device:
@@ -551,6 +617,7 @@ void Context::begin_eval(const int * tokens, int n, int n_past, const EvalPart &
     sh->n_past = n_past;
     sh->n_tokens = n;
     sh->pad0 = (n == 1 && model.has_embed) ? tokens[0] : 0;
+    sh->seq = next_seq();
     if (model.has_head && part.tok_off == 0)   // within the reserve: the pointer never moves
         logits.resize((size_t) (last_only ? 1 : n_total) * V);
     if (graph_ok) {

@@ -152,6 +152,19 @@ struct Context {
     int * greedy_h = nullptr;    // host-mapped (coherent): the device argmax writes it
     int * greedy_hd = nullptr;   // its device address
     void enqueue_argmax();
+    // chained greedy decode (lvk_decode_greedy): one graph per step that reads nothing from
+    // the host -- its last kernel (k_argmax_step) picks the token, advances the step block
+    // on the device and writes the next step's embedding row -- replayed n times per call
+    hipGraph_t graph_chain = nullptr;
+    hipGraphExec_t graph_chain_exec = nullptr;
+    int * chain_d = nullptr;     // [1 + n_ctx]: step counter, then the tokens
+    int * chain_h = nullptr;     // pinned copy of the tokens
+    int decode_greedy(int token, int n_past, int n_steps, int * out);
+    // decode attention granule epochs from the step counter (StepParams::seq): no zeroing per
+    // token (off for the fused attention + Wo kernel and models with more than 126 layers)
+    bool seq_epochs = false;
+    unsigned seq = 0;            // the last step counter handed to the device
+    unsigned next_seq(unsigned k = 1);
 
     // host-visible results
     std::vector<float, PinnedAlloc<float>> logits;
@@ -184,9 +197,10 @@ struct Context {
     void end_eval(bool no_host_logits);
     // stage boundary: copy the residual stream x [n][E] to (to_ctx) or from the context
     void x_copy(void * buf, int n, bool to_ctx, bool on_device);
-    void enqueue_forward(int n, bool last_only, const int * tok_src = nullptr, int logit_row = 0, bool head = true);
+    void enqueue_forward(int n, bool last_only, const int * tok_src = nullptr, int logit_row = 0, bool head = true,
+                         bool embed = true);
     bool use_mfma(int n) const;
-    void build_graph(int kind = 0);      // 0 logits, 1 greedy, 2 sample
+    void build_graph(int kind = 0);      // 0 logits, 1 greedy, 2 sample, 3 chained greedy step
     int eval_greedy(int token, int n_past);
     void kv_get();
     void kv_set(const uint8_t * src, size_t n);

@@ -401,4 +401,26 @@ int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past) {
     return r;
 }
 
+int lvk_decode_greedy(struct llama_context * ctx, int token, int n_past, int n_steps, int * out_tokens) {
+    if (!ctx || !out_tokens) {
+        fprintf(stderr, "%s: null argument\n", __func__);
+        return -1;
+    }
+    if (ctx->split) {
+        fprintf(stderr, "%s: not available on a layer split (use lvk_eval_greedy per step)\n", __func__);
+        return -1;
+    }
+    lvk::Context & c = ctx->c;
+    const int64_t t0 = lvk::now_us();
+    try {
+        c.decode_greedy(token, n_past, n_steps, out_tokens);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: failed to eval: %s\n", __func__, e.msg.c_str());
+        return -1;
+    }
+    c.t_eval_us += lvk::now_us() - t0;   // n_steps decode evals (llama.cpp:1186-1195)
+    c.n_eval += n_steps;
+    return 0;
+}
+
 }  // extern "C"

@@ -112,6 +112,7 @@ _sig("lvk_set_decode_persistent", None, [C.c_void_p, C.c_int])
 _sig("lvk_decode_persistent_active", C.c_int, [C.c_void_p])
 _sig("lvk_set_prompt_exact", None, [C.c_void_p, C.c_int])
 _sig("lvk_eval_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int])
+_sig("lvk_decode_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p])
 _sig("lvk_argmax", C.c_int, [f32p, C.c_int])
 _sig("lvk_sample_candidates", C.c_int, [f32p, C.c_int, i32p, C.c_int, C.c_int, C.c_float, C.c_float, f32p, i32p, C.POINTER(C.c_int)])
 _sig("lvk_kv_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_int])
@@ -190,6 +191,15 @@ class Llama:
         if r < 0:
             raise RuntimeError("lvk_eval_greedy failed")
         return r
+
+    def decode_greedy(self, token, n_past, n_steps):
+        """n_steps greedy decode steps on the device in one call (lvk_decode_greedy): the tokens
+        n_steps chained eval_greedy calls would return, as an int32 array"""
+        out = np.zeros(int(n_steps), np.int32)
+        r = lib.lvk_decode_greedy(self.ctx, int(token), int(n_past), int(n_steps), out.ctypes.data)
+        if r != 0:
+            raise RuntimeError("lvk_decode_greedy failed")
+        return out
 
     # ---- pipeline stage (lvk_init_stage contexts)
     def stage_eval(self, tokens, n_tokens, n_past):
