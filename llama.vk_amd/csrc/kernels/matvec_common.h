@@ -6,6 +6,24 @@
 namespace lvk {
 namespace mv {
 
+// Marks loaded values as produced here for hipcc's wait-count pass.  A load whose result is
+// first used after a branch join (e.g. the optional weight issue of a matvec prologue) is
+// otherwise waited for with the most conservative count of the two paths -- vmcnt(1) behind
+// a weight burst, i.e. the whole burst.  Passing the values through an empty asm statement
+// where the exact count is known (right after the burst, in each branch) puts the precise
+// wait there and none later.
+__device__ __forceinline__ void launder(float4 & v) {
+    float a = v.x, b = v.y, c = v.z, d = v.w;
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    v = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void launder(uint4 & v) {
+    uint32_t a = v.x, b = v.y, c = v.z, d = v.w;
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    v = make_uint4(a, b, c, d);
+}
+__device__ __forceinline__ void launder(float & v) { asm volatile("" : "+v"(v)); }
+
 // LDS activation table of one token:
 //   act[nb/4][8] uint4 : for 4 blocks 4u..4u+3 and chain j:
 //       {a(4u,j), a(4u+1,j) << 16, a(4u+2,j), a(4u+3,j) << 16}

@@ -102,6 +102,14 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
                     gv[k][0] = gp[0]; gv[k][1] = gp[1];
                 }
             }
+            constexpr int XPL = PRO == PRO_NORM ? KT / 4 / 64 : 1;
+            float4 xs[XPL];
+            if constexpr (PRO == PRO_NORM) {
+#pragma unroll
+                for (int i = 0; i < XPL; ++i) xs[i] = ((const float4 *) P.x)[i * 64 + lane];
+            }
+            // barrier A: the inputs enter the CU's texture queue ahead of the weight burst
+            __builtin_amdgcn_s_barrier();
             float scale = 1.0f;
             if constexpr (PRO == PRO_NORM) {
                 // ggml_compute_forward_rms_norm_f32 (ggml.c:6058-6076): every
@@ -109,10 +117,6 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
                 // butterfly that leaves the same double in every lane), so no
                 // cross-wave reduction is needed.  Terms are float squares
                 // carried in double (RMSNorm order).
-                constexpr int XPL = KT / 4 / 64;
-                float4 xs[XPL];
-#pragma unroll
-                for (int i = 0; i < XPL; ++i) xs[i] = ((const float4 *) P.x)[i * 64 + lane];
                 double acc = 0.0;
 #pragma unroll
                 for (int i = 0; i < XPL; ++i) {
@@ -155,6 +159,7 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
                 if (un < nunits) act_store(act, dxp, un >> 2, un & 3, w, d, (un & 3) == 0);
             }
         } else {
+            __builtin_amdgcn_s_barrier();       // barrier A (see above)
             constexpr int UMP = (nb + PT_ - 1) / PT_;
 #pragma unroll
             for (int k = 0; k < UMP; ++k) {
@@ -181,7 +186,7 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     const int g0 = (int) (blockIdx.x * (unsigned) P.G / (unsigned) nwg);     // G * n_cu < 2^32
     const int g1 = (int) ((blockIdx.x + 1) * (unsigned) P.G / (unsigned) nwg);
     const int ng = max(0, (g1 - g0 - wave + NW - 1) / NW);      // row groups of this wave
-    if (NP > 0 && ng == 0) { __syncthreads(); return; }
+    if (NP > 0 && ng == 0) { __builtin_amdgcn_s_barrier(); __syncthreads(); return; }
     int gc = min(g0 + wave, P.G - 1);
 
     // NP == 0: the compute waves build the activation table themselves; its
@@ -215,9 +220,28 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
         }
     }
 
+    // the prologue inputs, marked landed where the wait count is exact (matvec_common.h):
+    // hipcc then waits for exactly them, never for weight loads issued behind them
+    auto launder_inputs = [&]() __attribute__((always_inline)) {
+        if constexpr (NP == 0) {
+#pragma unroll
+            for (int k = 0; k < UM; ++k) {
+                if constexpr (FPRO) {
+                    launder(xv[k][0]); launder(xv[k][1]);
+                    if constexpr (PRO == PRO_NORM) { launder(gv[k][0]); launder(gv[k][1]); }
+                } else {
+                    launder(qv[k]); launder(dv[k]);
+                }
+            }
+        }
+    };
+
     // first D chunks of this wave's first row group (wave-uniform base +
-    // 32-bit lane offset: the scalar-base load form)
-    const uint32_t loff = (uint32_t) lane * 16u;
+    // 32-bit lane offset: the scalar-base load form).  A wave without row groups (it only
+    // helps build the table) issues the same loads with every lane on one 16-byte word:
+    // no branch around the issue, so hipcc's wait counts stay exact on every path.
+    const bool issue = NP > 0 || ng > 0;
+    const uint32_t loff = issue ? (uint32_t) lane * 16u : 0u;
     uint4 W[D][4];
     float4 S[D];
     // the scales of a chunk go out before its nibbles: the scale table of chunk c+1 is
@@ -231,23 +255,23 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
         __builtin_amdgcn_sched_barrier(0);                                                              \
     } while (0)
     // Order of the prologue and the first weight loads (PF):
-    //   0: weights first, then the activation table (the inputs land behind the burst);
+    //   0: the inputs, then the weights are issued, then the activation table is built as
+    //      soon as the inputs land (the weights stay in flight);
     //   1: the inputs land, then the weights are issued, then the table is built;
     //   2: the inputs land and the table is built, then the weights are issued;
     //   3: as 2, but the weights are issued after the workgroup barrier.
     // A CU's texture unit takes a 1 KiB wave load in ~16 cycles: issuing 80-160 KiB of
     // weights keeps every wave of the CU in its issue for 1.3-4k cycles, so with 0 or 1 the
-    // table (and the first chain) waits for the whole burst to be issued (tools/probe traces).
-    if constexpr (PF >= 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // table (and the first chain) waits for the wave's own share of the burst to be issued.
+    if constexpr (PF >= 1) launder_inputs();
+    // prologue waves (NP > 0): the weight burst goes out behind their inputs (barrier A)
+    if constexpr (NP > 0) __builtin_amdgcn_s_barrier();
     LVK_T(58);
-    // a wave without row groups issues no weight loads (it only helps build the table)
-    const bool issue = NP > 0 || ng > 0;
     if constexpr (PF <= 1) {
-        if (issue) {
 #pragma unroll
-            for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
-        }
+        for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
     }
+    if constexpr (PF == 0) launder_inputs();
     LVK_T(59);
 
     if constexpr (NP == 0) {
@@ -318,10 +342,8 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
         }
     }
     if constexpr (PF == 2) {
-        if (issue) {
 #pragma unroll
-            for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
-        }
+        for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
     }
     LVK_T(1);
     __syncthreads();            // activation table ready
@@ -539,11 +561,11 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         switch (cfg) { case 0: return go<a0, PR, E, K_>(P, s); case 1: return go<a1, PR, E, K_>(P, s); \
                        case 2: return go<a2, PR, E, K_>(P, s); default: return go<a3, PR, E, K_>(P, s); }
 #define C3(a, b, c) a, b, c
-        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(8, 0, 3), C3(8, 0, 4), C3(12, 0, 2))
-        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(12, 0, 3), C3(12, 0, 4), C3(16, 0, 2))
-        if (K == 4096 && epi == EPI_STORE) SW4(EPI_STORE, PRO_NORM, 4096, C3(16, 0, 2), C3(16, 0, 3), C3(12, 0, 2), C3(12, 0, 3))
-        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 0, 4), C3(4, 0, 2), C3(8, 0, 2))
-        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(4, 0, 4), C3(8, 0, 4), C3(16, 0, 4), C3(8, 0, 6))
+        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(8, 1, 2), C3(8, 2, 2), C3(8, 4, 2))
+        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(12, 1, 2), C3(12, 2, 2), C3(12, 4, 2))
+        if (K == 4096 && epi == EPI_STORE) SW4(EPI_STORE, PRO_NORM, 4096, C3(16, 0, 2), C3(15, 1, 2), C3(14, 2, 2), C3(12, 4, 2))
+        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 1, 2), C3(2, 2, 2), C3(4, 0, 2))
+        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(8, 0, 4), C3(2, 2, 4), C3(2, 6, 4), C3(2, 14, 4))
     }
 #endif
     // launch shapes (waves NW, prefetch depth D) per row length and role, measured on
@@ -551,7 +573,7 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
     // every CU keeps ~60-120 KB of weights in flight
     if (K == 4096) {
         switch (epi) {
-            case EPI_QKV: if (pro == PRO_NORM) return go<8, 0, 2, PRO_NORM, EPI_QKV, 4096, 2>(P, s); break;
+            case EPI_QKV: if (pro == PRO_NORM) return go<8, 0, 2, PRO_NORM, EPI_QKV, 4096, 1>(P, s); break;
             case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 4096, 1>(P, s); break;
             case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 4096, 1>(P, s); break;
             case EPI_RESID: if (pro == PRO_ACTQ) return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096, 2>(P, s); break;
@@ -567,8 +589,11 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         }
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 8192>(P, s);
     } else if (K == 11008) {
-        // 8 waves: the 6 without a row group help quantize u (tools/probe sweep r03: 8.0 vs 8.9 us)
-        if (epi == EPI_RESID && pro == PRO_ACTF) return go<8, 0, 4, PRO_ACTF, EPI_RESID, 11008, 2>(P, s);
+        // 2 compute waves (one row group each) put the weight burst in flight at once, behind
+        // the u loads of 6 prologue waves that quantize u meanwhile (tools/gpu_sweep_np.sh,
+        // profiles/r03_np_sweep.txt: 7.0 us against 8.6-9.3 for 8 waves that all quantize u
+        // and then issue the weights)
+        if (epi == EPI_RESID && pro == PRO_ACTF) return go<2, 6, 4, PRO_ACTF, EPI_RESID, 11008, 0>(P, s);
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 0, 4, PRO_ACTF, EPI_STORE, 11008>(P, s);
         if (epi == EPI_STORE && pro == PRO_NORM) return go<4, 0, 4, PRO_NORM, EPI_STORE, 11008>(P, s);
     } else if (K == 22016) {

@@ -318,14 +318,42 @@ __device__ inline ArgBest arg_pick(ArgBest a, ArgBest b) {
     if (a.i == INT_MAX) return b;
     return (b.v > a.v || (b.v == a.v && b.i < a.i)) ? b : a;
 }
+__device__ inline void arg_take(ArgBest & b, float v, int i) {
+    if (v == v && (b.i == INT_MAX || v > b.v)) b = {v, i};
+}
+// this thread's best over x[0..n): float4 slices t, t + 1024, ... with up to 8 of them in
+// flight per trip (a 32000-entry vocabulary is one trip), entries in increasing index order
+// per thread; unaligned or ragged inputs take the scalar stride
+__device__ inline ArgBest arg_scan(const float * __restrict__ x, int n) {
+    ArgBest b{-INFINITY, INT_MAX};
+    const int t = threadIdx.x;
+    if ((((uintptr_t) x) & 15) == 0 && (n & 3) == 0) {
+        const float4 * x4 = (const float4 *) x;
+        const int n4 = n >> 2;
+        constexpr int U = 8;
+        for (int base = 0; base < n4; base += U * 1024) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = base + u * 1024 + t;
+                v[u] = k < n4 ? x4[k] : make_float4(NAN, NAN, NAN, NAN);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = (base + u * 1024 + t) * 4;
+                arg_take(b, v[u].x, i); arg_take(b, v[u].y, i + 1);
+                arg_take(b, v[u].z, i + 2); arg_take(b, v[u].w, i + 3);
+            }
+        }
+    } else {
+        for (int i = t; i < n; i += 1024) arg_take(b, x[i], i);
+    }
+    return b;
+}
 __global__ __launch_bounds__(1024) void k_argmax_first(const float * __restrict__ x, int n, int * __restrict__ out,
                                                        int * __restrict__ out2) {
     __shared__ ArgBest red[16];
-    ArgBest b{-INFINITY, INT_MAX};
-    for (int i = threadIdx.x; i < n; i += 1024) {
-        const float v = x[i];
-        if (v == v && (b.i == INT_MAX || v > b.v)) b = {v, i};
-    }
+    ArgBest b = arg_scan(x, n);
     for (int off = 32; off > 0; off >>= 1) {
         ArgBest o;
         o.v = __shfl_xor(b.v, off, 64);
@@ -353,11 +381,7 @@ __global__ __launch_bounds__(1024) void k_argmax_step(const float * __restrict__
                                                       float * __restrict__ x) {
     __shared__ ArgBest red[16];
     __shared__ int s_tok;
-    ArgBest b{-INFINITY, INT_MAX};
-    for (int i = threadIdx.x; i < n; i += 1024) {
-        const float v = logits[i];
-        if (v == v && (b.i == INT_MAX || v > b.v)) b = {v, i};
-    }
+    ArgBest b = arg_scan(logits, n);
     for (int off = 32; off > 0; off >>= 1) {
         ArgBest o;
         o.v = __shfl_xor(b.v, off, 64);
