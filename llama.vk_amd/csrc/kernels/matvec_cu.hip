@@ -259,19 +259,26 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     //      soon as the inputs land (the weights stay in flight);
     //   1: the inputs land, then the weights are issued, then the table is built;
     //   2: the inputs land and the table is built, then the weights are issued;
-    //   3: as 2, but the weights are issued after the workgroup barrier.
+    //   3: as 2, but the weights are issued after the workgroup barrier;
+    //   4: as 0, but only chunk 0 goes out before the table, chunks 1..D-1 after the barrier
+    //      (the barriers wait for the slowest wave's issue, which the memory system throttles
+    //      to the return rate once the CU's queue is full);
+    //   5: as 4, but the inputs land before chunk 0 is issued.
     // A CU's texture unit takes a 1 KiB wave load in ~16 cycles: issuing 80-160 KiB of
     // weights keeps every wave of the CU in its issue for 1.3-4k cycles, so with 0 or 1 the
     // table (and the first chain) waits for the wave's own share of the burst to be issued.
-    if constexpr (PF >= 1) launder_inputs();
+    constexpr bool SPLIT = PF == 4 || PF == 5;
+    if constexpr (PF != 0 && PF != 4) launder_inputs();
     // prologue waves (NP > 0): the weight burst goes out behind their inputs (barrier A)
     if constexpr (NP > 0) __builtin_amdgcn_s_barrier();
     LVK_T(58);
     if constexpr (PF <= 1) {
 #pragma unroll
         for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
+    } else if constexpr (SPLIT) {
+        LVK_ISSUE(0, gc, 0);
     }
-    if constexpr (PF == 0) launder_inputs();
+    if constexpr (PF == 0 || PF == 4) launder_inputs();
     LVK_T(59);
 
     if constexpr (NP == 0) {
@@ -354,6 +361,9 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
         // as soon as they land (no workgroup barrier behind the issue)
 #pragma unroll
         for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
+    } else if constexpr (SPLIT) {
+#pragma unroll
+        for (int d = 1; d < D; ++d) LVK_ISSUE(d, gc, d);
     }
 
     // 4. row groups: chunk loop with cross-group prefetch.  Per chunk: the chunk's
@@ -504,7 +514,9 @@ hipError_t go(const CuParams & P, hipStream_t s) {
         case 0: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 0>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
         case 1: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 1>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
         case 2: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 2>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
-        default: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 3>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
+        case 3: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 3>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
+        case 4: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 4>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
+        default: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 5>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
     }
     return hipGetLastError();
 }
@@ -561,11 +573,12 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         switch (cfg) { case 0: return go<a0, PR, E, K_>(P, s); case 1: return go<a1, PR, E, K_>(P, s); \
                        case 2: return go<a2, PR, E, K_>(P, s); default: return go<a3, PR, E, K_>(P, s); }
 #define C3(a, b, c) a, b, c
-        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(8, 1, 2), C3(8, 2, 2), C3(8, 4, 2))
-        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(12, 1, 2), C3(12, 2, 2), C3(12, 4, 2))
-        if (K == 4096 && epi == EPI_STORE) SW4(EPI_STORE, PRO_NORM, 4096, C3(16, 0, 2), C3(15, 1, 2), C3(14, 2, 2), C3(12, 4, 2))
-        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 1, 2), C3(2, 2, 2), C3(4, 0, 2))
-        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(8, 0, 4), C3(2, 2, 4), C3(2, 6, 4), C3(2, 14, 4))
+        if (K == 4096 && epi == EPI_QKV) SW4(EPI_QKV, PRO_NORM, 4096, C3(8, 0, 2), C3(8, 0, 4), C3(12, 0, 2), C3(6, 0, 4))
+        if (K == 4096 && epi == EPI_SWIGLU_F32) SW4(EPI_SWIGLU_F32, PRO_NORM, 4096, C3(12, 0, 2), C3(12, 0, 4), C3(16, 0, 2), C3(8, 0, 4))
+        if (K == 4096 && epi == EPI_STORE) SW4(EPI_STORE, PRO_NORM, 4096, C3(16, 0, 2), C3(16, 0, 4), C3(12, 0, 4), C3(8, 0, 4))
+        if (K == 4096 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTQ, 4096, C3(2, 0, 2), C3(2, 0, 4), C3(4, 0, 2), C3(4, 0, 4))
+        if (K == 11008) SW4(EPI_RESID, PRO_ACTF, 11008, C3(2, 6, 4), C3(2, 6, 2), C3(2, 10, 4), C3(2, 4, 4))
+        if (K == 22016 && epi == EPI_RESID) SW4(EPI_RESID, PRO_ACTF, 22016, C3(4, 0, 2), C3(4, 12, 2), C3(4, 4, 2), C3(4, 8, 2))
     }
 #endif
     // launch shapes (waves NW, prefetch depth D) per row length and role, measured on
