@@ -586,10 +586,12 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
     // every CU keeps ~60-120 KB of weights in flight
     if (K == 4096) {
         switch (epi) {
-            case EPI_QKV: if (pro == PRO_NORM) return go<8, 0, 2, PRO_NORM, EPI_QKV, 4096, 1>(P, s); break;
-            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 4096, 1>(P, s); break;
+            // prologue order 5 (inputs, chunk 0, table, the rest after the barrier): QKV 7.6 vs
+            // 7.7-8.4 us, Wo 4.4 vs 4.5-4.9 over orders 0-2 (profiles/r03_pf_sweep.txt)
+            case EPI_QKV: if (pro == PRO_NORM) return go<8, 0, 2, PRO_NORM, EPI_QKV, 4096, 5>(P, s); break;
+            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 4096, 5>(P, s); break;
             case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 4096, 1>(P, s); break;
-            case EPI_RESID: if (pro == PRO_ACTQ) return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096, 2>(P, s); break;
+            case EPI_RESID: if (pro == PRO_ACTQ) return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096, 5>(P, s); break;
         }
         // operator API (lvk_mul_mat_q: plain quantize of an f32 input)
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 4096>(P, s);
@@ -610,7 +612,8 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 0, 4, PRO_ACTF, EPI_STORE, 11008>(P, s);
         if (epi == EPI_STORE && pro == PRO_NORM) return go<4, 0, 4, PRO_NORM, EPI_STORE, 11008>(P, s);
     } else if (K == 22016) {
-        if (epi == EPI_RESID && pro == PRO_ACTF) return go<4, 0, 2, PRO_ACTF, EPI_RESID, 22016>(P, s);
+        // 4 compute + 8 prologue waves (the 11008 rule): 20.0 vs 22.1 us (profiles/r03_sweep65.txt)
+        if (epi == EPI_RESID && pro == PRO_ACTF) return go<4, 8, 2, PRO_ACTF, EPI_RESID, 22016, 0>(P, s);
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 0, 2, PRO_ACTF, EPI_STORE, 22016>(P, s);
         if (epi == EPI_STORE && pro == PRO_NORM) return go<4, 0, 2, PRO_NORM, EPI_STORE, 22016>(P, s);
     }
