@@ -52,7 +52,10 @@ struct Cu41Params {
 // bank-conflict free (a 32-float stride put rows 0/2/4/6 on the same banks)
 constexpr int SRS = 40, SPL = 8 * SRS, SWF = 4 * SPL;
 
-template <int NW, int D, int PRO, int EPI, int KT>
+// SPLIT: only chunk 0 goes out before the activation table, chunks 1..D-1 after the workgroup
+// barrier (the barriers wait for the slowest wave's issue, which the memory system throttles
+// to the return rate once the CU's queue is full; matvec_cu.hip prologue order 5)
+template <int NW, int D, int PRO, int EPI, int KT, int SPLIT = 0>
 __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     constexpr int nb = KT / 32;                 // blocks per row
     constexpr int nsub = nb / 8;                // 8-block sub-chunks (one uint4 per lane each)
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
         __builtin_amdgcn_sched_barrier(0);                                                              \
     } while (0)
 #pragma unroll
-    for (int d = 0; d < D; ++d) LVK_ISSUE41(d, gc, d);
+    for (int d = 0; d < (SPLIT ? 1 : D); ++d) LVK_ISSUE41(d, gc, d);
 
     // activation table
     if constexpr (FPRO) {
@@ -191,6 +194,10 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     }
     __syncthreads();            // activation table ready
     if (ng == 0) return;
+    if constexpr (SPLIT) {
+#pragma unroll
+        for (int d = 1; d < D; ++d) LVK_ISSUE41(d, gc, d);
+    }
 
     // row groups: chunk loop with cross-group prefetch
     const bool even = (j & 1) == 0;
@@ -326,7 +333,7 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
 #undef LVK_ISSUE41
 }
 
-template <int NW, int D, int PRO, int EPI, int KT>
+template <int NW, int D, int PRO, int EPI, int KT, int SPLIT = 0>
 hipError_t go(const Cu41Params & P, hipStream_t s) {
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
     constexpr bool XG = (NC % D) == 0;
@@ -334,7 +341,7 @@ hipError_t go(const Cu41Params & P, hipStream_t s) {
     // without cross-group prefetch every wave must own at most one group
     if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
     const size_t lds = (size_t) nb * 32 + 2 * NC * 128 + (size_t) nb * 16 + NW * SWF * 4 + NW * 8;
-    LVK_LAUNCH((k_mv_cu41<NW, D, PRO, EPI, KT>), dim3(nwg), dim3(NW * 64), lds, s, P);
+    LVK_LAUNCH((k_mv_cu41<NW, D, PRO, EPI, KT, SPLIT>), dim3(nwg), dim3(NW * 64), lds, s, P);
     return hipGetLastError();
 }
 
@@ -368,29 +375,22 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
     {
         static int cfg = getenv("LVK_CFG41") ? atoi(getenv("LVK_CFG41")) : 0;
         if (K == 5120 && epi == EPI_QKV) {
-            if (cfg == 1) return go<8, 1, PRO_NORM, EPI_QKV, 5120>(P, s);
-            if (cfg == 2) return go<4, 5, PRO_NORM, EPI_QKV, 5120>(P, s);
-            if (cfg == 3) return go<8, 5, PRO_NORM, EPI_QKV, 5120>(P, s);
+            if (cfg == 1) return go<8, 2, PRO_NORM, EPI_QKV, 5120, 1>(P, s);
+            if (cfg == 2) return go<8, 1, PRO_NORM, EPI_QKV, 5120>(P, s);
+            if (cfg == 3) return go<6, 5, PRO_NORM, EPI_QKV, 5120, 1>(P, s);
         }
         if (K == 5120 && epi == EPI_SWIGLU_F32) {
-            if (cfg == 1) return go<7, 5, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
-            if (cfg == 2) return go<8, 1, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
-            if (cfg == 3) return go<4, 5, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s);
+            if (cfg == 3) return go<6, 5, PRO_NORM, EPI_SWIGLU_F32, 5120, 1>(P, s);
         }
         if (K == 5120 && epi == EPI_RESID) {
-            if (cfg == 1) return go<3, 5, PRO_ACTQ, EPI_RESID, 5120>(P, s);
-            if (cfg == 2) return go<3, 1, PRO_ACTQ, EPI_RESID, 5120>(P, s);
-            if (cfg == 3) return go<4, 2, PRO_ACTQ, EPI_RESID, 5120>(P, s);
+            if (cfg == 1) return go<3, 2, PRO_ACTQ, EPI_RESID, 5120, 1>(P, s);
+            if (cfg == 3) return go<3, 5, PRO_ACTQ, EPI_RESID, 5120, 1>(P, s);
         }
         if (K == 13824 && epi == EPI_RESID) {
-            if (cfg == 1) return go<4, 7, PRO_ACTF, EPI_RESID, 13824>(P, s);
-            if (cfg == 2) return go<8, 2, PRO_ACTF, EPI_RESID, 13824>(P, s);
-            if (cfg == 3) return go<4, 14, PRO_ACTF, EPI_RESID, 13824>(P, s);
+            if (cfg == 1) return go<8, 2, PRO_ACTF, EPI_RESID, 13824, 1>(P, s);
         }
         if (K == 5120 && epi == EPI_STORE && pro == PRO_NORM) {
-            if (cfg == 1) return go<8, 1, PRO_NORM, EPI_STORE, 5120>(P, s);
-            if (cfg == 2) return go<4, 5, PRO_NORM, EPI_STORE, 5120>(P, s);
-            if (cfg == 3) return go<6, 5, PRO_NORM, EPI_STORE, 5120>(P, s);
+            if (cfg == 3) return go<6, 5, PRO_NORM, EPI_STORE, 5120, 1>(P, s);
         }
     }
 #endif
@@ -402,7 +402,9 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
     // at D = 5 and 29.3 for 14 waves, lm_head 27.4 vs 30.1)
     if (K == 5120) {
         switch (epi) {
-            case EPI_QKV: if (pro == PRO_NORM) return go<8, 2, PRO_NORM, EPI_QKV, 5120>(P, s); break;
+            // SPLIT (chunk 1 after the table barrier): 16.9 vs 17.5 us, W2 19.5 vs 19.8
+            // (profiles/r03_sweep13_split.txt)
+            case EPI_QKV: if (pro == PRO_NORM) return go<8, 2, PRO_NORM, EPI_QKV, 5120, 1>(P, s); break;
             case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<8, 1, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s); break;
             case EPI_STORE:
                 if (pro == PRO_NORM) return go<8, 1, PRO_NORM, EPI_STORE, 5120>(P, s);
@@ -413,7 +415,7 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
     } else if (K == 13824) {
         // 8 waves: the 5-6 without a row group help quantize u (r03 sweep: 19.9 vs 20.9 us;
         // D = 7 / 14 with 4 waves: 23.5 / 28.3)
-        if (epi == EPI_RESID && pro == PRO_ACTF) return go<8, 2, PRO_ACTF, EPI_RESID, 13824>(P, s);
+        if (epi == EPI_RESID && pro == PRO_ACTF) return go<8, 2, PRO_ACTF, EPI_RESID, 13824, 1>(P, s);
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 2, PRO_ACTF, EPI_STORE, 13824>(P, s);
     } else if (K == 4096) {
         switch (epi) {
