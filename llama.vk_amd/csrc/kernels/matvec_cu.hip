@@ -597,10 +597,12 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 4096>(P, s);
     } else if (K == 8192) {
         switch (epi) {
-            case EPI_QKV: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_QKV, 8192>(P, s); break;
-            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 8192>(P, s); break;
+            // prologue orders on the 65B shapes (tools/gpu_pf65.sh, profiles/r03_pf65.txt): 0 for
+            // QKV / W1|W3 (22.4 / 38.6 vs 23.1 / 40.1 us at order 2), 5 for Wo (8.2 vs 8.4)
+            case EPI_QKV: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_QKV, 8192, 0>(P, s); break;
+            case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 8192, 0>(P, s); break;
             case EPI_STORE: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_STORE, 8192>(P, s); break;
-            case EPI_RESID: if (pro == PRO_ACTQ) return go<4, 0, 2, PRO_ACTQ, EPI_RESID, 8192>(P, s); break;
+            case EPI_RESID: if (pro == PRO_ACTQ) return go<4, 0, 2, PRO_ACTQ, EPI_RESID, 8192, 5>(P, s); break;
         }
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 8192>(P, s);
     } else if (K == 11008) {
