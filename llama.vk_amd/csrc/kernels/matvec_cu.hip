@@ -610,7 +610,13 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         // the u loads of 6 prologue waves that quantize u meanwhile (tools/gpu_sweep_np.sh,
         // profiles/r03_np_sweep.txt: 7.0 us against 8.6-9.3 for 8 waves that all quantize u
         // and then issue the weights)
-        if (epi == EPI_RESID && pro == PRO_ACTF) return go<2, 6, 4, PRO_ACTF, EPI_RESID, 11008, 0>(P, s);
+        if (epi == EPI_RESID && pro == PRO_ACTF) {
+            // (needs at most 2 row groups per CU: a device with fewer CUs takes 8 waves that
+            // all quantize u, then issue the weights)
+            const hipError_t e = go<2, 6, 4, PRO_ACTF, EPI_RESID, 11008, 0>(P, s);
+            if (e != hipErrorNotSupported) return e;
+            return go<8, 0, 4, PRO_ACTF, EPI_RESID, 11008, 2>(P, s);
+        }
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 0, 4, PRO_ACTF, EPI_STORE, 11008>(P, s);
         if (epi == EPI_STORE && pro == PRO_NORM) return go<4, 0, 4, PRO_NORM, EPI_STORE, 11008>(P, s);
     } else if (K == 22016) {
