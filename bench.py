@@ -164,10 +164,45 @@ def ensure_model(path, coord, cfg):
     coord.barrier()
 
 
+def cpu_quota():
+    """CPUs this process may use per the cgroup CPU controller (v2 cpu.max, v1
+    cpu.cfs_quota_us / cpu.cfs_period_us): (cpus or None when unlimited, where it was read)"""
+    try:
+        lines = open("/proc/self/cgroup").read().splitlines()
+    except OSError:
+        return None, "no /proc/self/cgroup"
+    for ln in lines:
+        parts = ln.split(":", 2)
+        if len(parts) != 3:
+            continue
+        hier, ctrls, path = parts
+        cands = []
+        if hier == "0" and ctrls == "":
+            cands = [("/sys/fs/cgroup" + path.rstrip("/") + "/cpu.max", "v2"), ("/sys/fs/cgroup/cpu.max", "v2")]
+        elif "cpu" in ctrls.split(","):
+            for root in ("/sys/fs/cgroup/cpu,cpuacct", "/sys/fs/cgroup/cpu"):
+                cands.append((root + path.rstrip("/") + "/cpu.cfs_quota_us", "v1"))
+                cands.append((root + "/cpu.cfs_quota_us", "v1"))
+        for f, kind in cands:
+            try:
+                if kind == "v2":
+                    q, per = open(f).read().split()[:2]
+                    return (None if q == "max" else float(q) / float(per)), f
+                q = int(open(f).read())
+                per = int(open(f.replace("cfs_quota_us", "cfs_period_us")).read())
+                return (None if q < 0 else q / per), f
+            except (OSError, ValueError):
+                continue
+    return None, "no cpu controller limit found"
+
+
 def cpu_info():
     """host CPU facts for the baseline line: nproc, model, AVX flags,
-    physical cores of this process's CPU set"""
+    physical cores of this process's CPU set, the cgroup CPU quota"""
     info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    q, src = cpu_quota()
+    info["cgroup_cpu_quota"] = q
+    info["cgroup_cpu_quota_source"] = src
     try:
         txt = open("/proc/cpuinfo").read()
         for line in txt.splitlines():
@@ -191,10 +226,11 @@ def cpu_info():
 
 def cpu_baseline(path, budget_s=20.0, label="7B Q4_0", prompt=True, seg_steps=16, n_seg=3):
     """The reference AVX2 ggml.c build (oracle/_ref/libref.so) on the same file and tokens:
-    decode tok/s (best of up to n_seg segments) at -t = the physical cores of this process's
-    CPU set (BASELINE.md section 4) and at the box's per-GPU share (OMP_NUM_THREADS, 16);
-    value = the faster of the two, and (prompt=True) the 512-token prompt batch at that
-    thread count -- llama.cpp:1186-1195's n_eval / t_eval and n_p_eval / t_p_eval."""
+    decode tok/s, best of n_seg segments, at two thread counts -- the usable cores (the
+    physical cores of this process's CPU set, capped by the cgroup CPU quota) and the box's
+    per-GPU share (OMP_NUM_THREADS, 16) -- each with its own half of the budget; value = the
+    faster, and (prompt=True) the 512-token prompt batch at that thread count, best of 3 --
+    llama.cpp:1186-1195's n_eval / t_eval and n_p_eval / t_p_eval."""
     from oracle_lib import REF_SO, Ref
     if not os.path.exists(REF_SO):
         return None
@@ -202,52 +238,69 @@ def cpu_baseline(path, budget_s=20.0, label="7B Q4_0", prompt=True, seg_steps=16
     info = cpu_info()
     share = int(os.environ.get("OMP_NUM_THREADS") or 0) or 16
     phys = info.get("physical_cores") or info["affinity"]
-    tried = []
-    for t in sorted({phys, min(share, phys)}, reverse=True):
-        tried.append(max(1, t))
+    usable = phys
+    if info.get("cgroup_cpu_quota"):
+        usable = max(1, min(phys, int(info["cgroup_cpu_quota"])))
+    tried = sorted({max(1, usable), max(1, min(share, usable))}, reverse=True)
     ref = Ref()
     t_load = time.perf_counter()
     m = ref.model(path, 512)
     t_load = time.perf_counter() - t_load
     toks = np.array(prompt_tokens(16), np.int32)
-    rates, t_used, n_past = {}, 0.0, 16
-    tok = 0
+    # a 2-step probe per thread count: a count far slower than the best (an oversubscribed
+    # quota the cgroup files do not show) is reported, not given segments
+    probe = {}
+    for threads in tried:
+        lg = m.eval(toks, 0, n_threads=threads)
+        tok = int(np.argmax(lg[-1]))
+        t0 = time.perf_counter()
+        for i in range(2):
+            lg = m.eval(np.array([tok], np.int32), 16 + i, n_threads=threads)
+            tok = int(np.argmax(lg[-1]))
+        probe[threads] = 2 / (time.perf_counter() - t0)
+    slow = [t for t in tried if probe[t] < max(probe.values()) / 3]
+    tried = [t for t in tried if t not in slow]
+    rates = {}
+    per_threads = (budget_s * (0.6 if prompt else 1.0)) / len(tried)
     for threads in tried:
         lg = m.eval(toks, 0, n_threads=threads)
         tok, n_past = int(np.argmax(lg[-1])), 16
-        segs = []
-        for _ in range(n_seg):
+        segs, used = [], 0.0
+        for k in range(n_seg):
             t0 = time.perf_counter()
             for _ in range(seg_steps):
                 lg = m.eval(np.array([tok], np.int32), n_past, n_threads=threads)
                 tok = int(np.argmax(lg[-1]))
-                n_past += 1
+                n_past = n_past + 1 if n_past + 1 < 512 else 16
             dt = time.perf_counter() - t0
             segs.append(seg_steps / dt)
-            t_used += dt
-            if t_used > budget_s / 2:
+            used += dt
+            # a segment that would overrun this thread count's budget is not started
+            if k + 1 < n_seg and used + dt > per_threads:
                 break
         rates[threads] = segs
     best_t = max(rates, key=lambda t: max(rates[t]))
     p512 = np.array(prompt_tokens(512), np.int32)
     pr = []
-    for _ in range(3 if prompt else 0):                      # 512-token prompt batch, best of up to 3
+    for _ in range(3 if prompt else 0):                      # 512-token prompt batch, best of 3
         t0 = time.perf_counter()
         m.eval(p512, 0, n_threads=best_t)
         pr.append(512 / (time.perf_counter() - t0))
-        t_used += 512 / pr[-1]
-        if t_used > budget_s:
+        if sum(512 / r for r in pr) > budget_s * 0.4 and len(pr) < 3:
             break
     m.close()
     out = {"value": max(rates[best_t]), "unit": "tok/s", "cores": best_t, "kind": "reference",
            "sample": "reference ggml.c AVX2 build (oracle/_ref, compiled from the reference sources), the same "
-                     "synthetic %s file and tokens, n_ctx 512, f16 KV: 16-token prompt, then segments of %d "
-                     "greedy decode steps at -t %s (physical cores of the CPU set, and the per-GPU share); "
-                     "value = the faster thread count (-t %d)%s"
-                     % (label, seg_steps, " and ".join(str(t) for t in tried), best_t,
+                     "synthetic %s file and tokens, n_ctx 512, f16 KV: 16-token prompt, then up to %d segments of "
+                     "%d greedy decode steps at each of -t %s (the usable cores: physical cores of the CPU set "
+                     "capped by the cgroup quota; and the per-GPU share), each thread count with its own budget; "
+                     "value = the best segment at the faster thread count (-t %d)%s"
+                     % (label, n_seg, seg_steps, " and ".join(str(t) for t in tried), best_t,
                         "; prompt = one 512-token batch at -t %d, best of %d" % (best_t, len(pr)) if prompt else ""),
            "decode_tok_s_by_threads": {str(t): max(v) for t, v in rates.items()},
-           "decode_segments_tok_s": rates[best_t], "load_s": t_load, "host": info}
+           "decode_segments_by_threads": {str(t): v for t, v in rates.items()},
+           "decode_segments_tok_s": rates[best_t], "probe_tok_s_by_threads": {str(t): v for t, v in probe.items()},
+           "dropped_slow_thread_counts": slow, "load_s": t_load, "host": info}
     if prompt:
         out["prompt_tok_s"] = max(pr)
         out["prompt_runs_tok_s"] = pr
@@ -255,13 +308,15 @@ def cpu_baseline(path, budget_s=20.0, label="7B Q4_0", prompt=True, seg_steps=16
 
 
 SPLIT_TIMEOUT_S = 420
+SPLIT_FIRST_TOKEN = 1000       # the greedy token the split's first decode step embeds
 
 
 def split_child(args):
     """one pipeline stage in a child process (bench.py --split-child): the C++ stage link
     (lvk_stage_connect / lvk_stage_step: ncclRecv -> this stage's layers -> ncclSend on the
-    stage's stream, greedy token relayed from the last stage to the first).  Prints one
-    JSON line."""
+    stage's stream, greedy token relayed from the last stage to the first; or the same over
+    the host shared-memory ring, --split-transport shm, for stages sharing a GPU).  Prints
+    one JSON line."""
     import numpy as np
     import lvk
     S, s = args.split_stages, args.split_stage
@@ -272,17 +327,23 @@ def split_child(args):
     t0 = time.time()
     st = lvk.Llama(args.split_model, n_ctx=512, layers=lr)
     load_s = time.time() - t0
-    st.stage_connect(bytes.fromhex(args.split_uid), S, s)
+    if args.split_transport == "shm":
+        st.stage_connect_shm(args.split_uid, S, s)
+    else:
+        st.stage_connect(bytes.fromhex(args.split_uid), S, s)
     ptoks = np.array(prompt_tokens(16), np.int32)
     first = s == 0
     st.stage_step(ptoks if first else None, 16, 0, micro=args.split_micro)
-    tok, n_past = 1000, 16
+    tok, n_past = SPLIT_FIRST_TOKEN, 16
+    toks = []
     for _ in range(args.warmup):
         tok = st.stage_step(np.array([tok], np.int32) if first else None, 1, n_past, greedy=True)
+        toks.append(tok)
         n_past += 1
     t0 = time.perf_counter()
     for _ in range(args.steps_split):
         tok = st.stage_step(np.array([tok], np.int32) if first else None, 1, n_past, greedy=True)
+        toks.append(tok)
         n_past = n_past + 1 if n_past + 1 < 512 else 16
     dec = time.perf_counter() - t0
     # a 512-token prompt through the pipeline, with and without micro-batches (every rank
@@ -299,24 +360,45 @@ def split_child(args):
         pre[micro] = best
     st.close()
     print(json.dumps({"stage": s, "layers": list(lr), "load_s": load_s, "decode_s": dec,
-                      "prefill_s": pre[args.split_micro], "prefill_nomicro_s": pre[0]}), flush=True)
+                      "prefill_s": pre[args.split_micro], "prefill_nomicro_s": pre[0],
+                      "tokens": toks if first else None}), flush=True)
+
+
+def greedy_tokens_1gpu(path, n):
+    """the same greedy steps as a split's stages (16-token prompt, then SPLIT_FIRST_TOKEN at
+    n_past 16, ...) on one unsplit context: what the split's token stream must equal"""
+    import numpy as np
+    import lvk
+    m = lvk.Llama(path, n_ctx=512)
+    m.eval(np.array(prompt_tokens(16), np.int32), 0)
+    tok, out = SPLIT_FIRST_TOKEN, []
+    for i in range(n):
+        tok = m.eval_greedy(tok, 16 + i)
+        out.append(tok)
+    m.close()
+    return out
 
 
 def layer_split(args, coord):
     """N > 1: LLaMA-65B Q4_0 (BASELINE configs[4]) split by layers over the ws ranks, one
-    stage per GPU, residual stream over RCCL send/recv (the C++ stage link).  Each rank runs
-    its stage in a child process under a time limit, so a transport failure costs this line,
-    not the bench."""
+    stage per GPU, residual stream over RCCL send/recv (the C++ stage link; --split-transport
+    shm: the host shared-memory ring, so that the ranks of a one-GPU rehearsal can share the
+    device).  Each rank runs its stage in a child process under a time limit, so a transport
+    failure costs this line, not the bench.  Rank 0 then replays the first --split-check
+    greedy steps on one unsplit context: the split's tokens must be the same."""
     path = args.split_model or os.path.join(os.path.dirname(args.model), "llama-65b-q4_0.bin")
     rank, ws, local = coord.rank, coord.ws, coord.local
     ensure_model(path, coord, CFG_65B)
     import lvk
-    # the communicator id is made here, in a process without torch (PipeCoord)
-    uid = [coord.bcast(lvk.rccl_unique_id().hex() if rank == 0 else None)]
+    # the communicator id (or the shm ring's name) is made here, in a process without torch
+    if args.split_transport == "shm":
+        uid = coord.bcast("/lvk_bench_%d_%s" % (os.getpid(), os.urandom(6).hex()) if rank == 0 else None)
+    else:
+        uid = coord.bcast(lvk.rccl_unique_id().hex() if rank == 0 else None)
     cmd = [sys.executable, os.path.abspath(__file__), "--split-child", "--split-stages", str(ws),
-           "--split-stage", str(rank), "--split-device", str(local % lvk.device_count()), "--split-uid", uid[0],
+           "--split-stage", str(rank), "--split-device", str(local % lvk.device_count()), "--split-uid", uid,
            "--split-model", path, "--steps-split", str(args.steps_split), "--warmup", "4",
-           "--split-micro", str(args.split_micro)]
+           "--split-micro", str(args.split_micro), "--split-transport", args.split_transport]
     res, err = None, None
     try:
         p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=SPLIT_TIMEOUT_S)
@@ -328,23 +410,38 @@ def layer_split(args, coord):
         err = "rank %d stage timed out after %d s" % (rank, SPLIT_TIMEOUT_S)
     except Exception as e:                       # noqa: BLE001 -- reported in the line
         err = "rank %d: %r" % (rank, e)
+    finally:
+        if args.split_transport == "shm" and rank == 0 and os.path.exists("/dev/shm" + uid):
+            os.unlink("/dev/shm" + uid)         # a stage that died before every stage joined
     ok = coord.max(0.0 if res is not None else 1.0) == 0.0
     if not ok:
-        return {"error": err or "another rank's stage failed"}
+        return {"error": err or "another rank's stage failed", "transport": args.split_transport}
     dec = coord.max(res["decode_s"])
     pre = coord.max(res["prefill_s"])
     pre0 = coord.max(res["prefill_nomicro_s"])
+    check = None
+    if rank == 0 and args.split_check > 0:
+        n = min(args.split_check, len(res["tokens"]))
+        t0 = time.time()
+        want = greedy_tokens_1gpu(path, n)
+        check = {"n_tokens": n, "tokens_split": res["tokens"][:n], "tokens_1gpu": want,
+                 "match": res["tokens"][:n] == want, "check_s": time.time() - t0,
+                 "positions": "16..%d" % (16 + n - 1), "first_token": SPLIT_FIRST_TOKEN}
+    coord.barrier()
     L = CFG_65B["n_layer"]
     r = args.steps_split / dec
+    transport = ("RCCL (ncclCommInitRank over the %d ranks)" % ws if args.split_transport == "rccl" else
+                 "host shared-memory ring (lvk_stage_connect_shm; the one-GPU rehearsal of the RCCL link)")
     return {"value": r, "unit": "tok/s", "stages": ws, "steps": args.steps_split, "ms_per_token": 1e3 / r,
             "layers_per_stage": [[s * L // ws, (s + 1) * L // ws] for s in range(ws)],
-            "workload": "LLaMA-65B Q4_0 (synthetic, seed 3) greedy decode, layers split over %d GPUs (one stage "
-                        "per rank, C++ stage link: ncclRecv -> layers -> ncclSend of inpL f32 [n_embd] on the "
-                        "stage stream, greedy token relayed last -> first by ncclSend), n_ctx 512" % ws,
+            "workload": "LLaMA-65B Q4_0 (synthetic, seed 3) greedy decode, layers split over %d stages (one "
+                        "stage per rank: recv -> layers -> send of inpL f32 [n_embd] on the stage stream, greedy "
+                        "token relayed last -> first), n_ctx 512" % ws,
             "frac_hbm_roofline_1gpu": r * MODEL_BYTES_65B / 1e9 / HBM_PEAK_GBS,
             "prefill_512": {"tok_s": 512 / pre, "ms": pre * 1e3, "micro_batch": args.split_micro,
                             "tok_s_no_micro_batch": 512 / pre0},
-            "transport": "RCCL (ncclCommInitRank over the %d ranks)" % ws}
+            "transport": transport, "devices": "rank r on device LOCAL_RANK %% %d" % lvk.device_count(),
+            "greedy_check": check}
 
 
 def decode_65b(args, coord, n_ctx, ptoks):
@@ -376,6 +473,13 @@ def decode_65b(args, coord, n_ctx, ptoks):
         tok = int(np.argmax(m.eval([tok], 16 + i * 60)[-1]))
     prof = m.profile()
     m.set_profiling(False)
+    # the greedy steps a layer split's stages run (layer_split's greedy_check): 16-token
+    # prompt, then SPLIT_FIRST_TOKEN at n_past 16, ...
+    m.eval(ptoks, 0)
+    tok, check = SPLIT_FIRST_TOKEN, []
+    for i in range(16):
+        tok = m.eval_greedy(tok, 16 + i)
+        check.append(tok)
     # 1-GPU 65B 512-token prompt (best of 2): the S = 1 reference point of the split's prefill
     ptoks512 = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, n_ctx)], np.int32)
     best = 1e30
@@ -405,6 +509,7 @@ def decode_65b(args, coord, n_ctx, ptoks):
             "frac_hbm_roofline": r * MODEL_BYTES_65B / 1e9 / HBM_PEAK_GBS,
             "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_65B,
             "kernels": kernels, "gen_s": gen_s, "load_s": load_s, "cpu_baseline": cpu65,
+            "greedy_check_tokens": check,
             "vs_cpu_baseline": (r / cpu65["value"]) if cpu65 else None}
 
 
@@ -427,6 +532,11 @@ def main():
     ap.add_argument("--steps-split", type=int, default=48)
     ap.add_argument("--split-model", default=None, help="model for the layer-split line (default: the 65B file)")
     ap.add_argument("--split-micro", type=int, default=64, help="prompt micro-batch of the layer split (tokens)")
+    ap.add_argument("--split-transport", choices=("rccl", "shm"), default="rccl",
+                    help="stage link of the layer split: RCCL (one GPU per rank, the default) or the host "
+                         "shared-memory ring (ranks may share a GPU: the one-GPU rehearsal)")
+    ap.add_argument("--split-check", type=int, default=16,
+                    help="greedy steps of the split replayed on one unsplit context by rank 0 (0: none)")
     ap.add_argument("--split-rehearse", action="store_true",
                     help="run the layer-split leg at N = 1 too (one stage: the RCCL link on one rank)")
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)

@@ -283,13 +283,26 @@ LVK_GGML_API void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgra
 LVK_GGML_API void ggml_graph_reset(struct ggml_cgraph * cgraph);
 LVK_GGML_API void ggml_graph_print(const struct ggml_cgraph * cgraph);
 
-/* ggml.h:783-793: system info (the host CPU's SIMD, as the reference reports it) */
+/* ggml.h:779-790: system info (the host CPU's SIMD, as the reference reports it) */
 LVK_GGML_API int ggml_cpu_has_avx(void);
 LVK_GGML_API int ggml_cpu_has_avx2(void);
 LVK_GGML_API int ggml_cpu_has_avx512(void);
 LVK_GGML_API int ggml_cpu_has_fma(void);
+LVK_GGML_API int ggml_cpu_has_neon(void);
+LVK_GGML_API int ggml_cpu_has_arm_fma(void);
 LVK_GGML_API int ggml_cpu_has_f16c(void);
+LVK_GGML_API int ggml_cpu_has_fp16_va(void);
+LVK_GGML_API int ggml_cpu_has_wasm_simd(void);
 LVK_GGML_API int ggml_cpu_has_blas(void);
+LVK_GGML_API int ggml_cpu_has_sse3(void);
+LVK_GGML_API int ggml_cpu_has_vsx(void);
+
+/* ggml.h:772-773 (ggml.c:10520-10564): the file-creation quantizers (quantize_row_q4_0/1
+ * _reference: roundf, half away from zero) over n values in rows of k, the 16-bin nibble
+ * histogram accumulated into hist; returns the bytes written (n/32 blocks).  Host code:
+ * llama_model_quantize and the reference's tests/test-quantize.c call them without a GPU. */
+LVK_GGML_API size_t ggml_quantize_q4_0(const float * src, void * dst, int n, int k, int64_t * hist);
+LVK_GGML_API size_t ggml_quantize_q4_1(const float * src, void * dst, int n, int k, int64_t * hist);
 
 /* ggml.h:796-814: the op-level codec table, same names, signatures and block layouts
  * (block_q4_0 {float d; uint8 qs[16]}, block_q4_1 {float d, m; uint8 qs[16]}).  Every

@@ -191,15 +191,37 @@ LVK_API int lvk_stage_layers(struct llama_context * ctx, int * layer_begin, int 
  * (reference llama.cpp:927-1197). */
 LVK_API int lvk_rccl_unique_id(void * id, size_t n);
 LVK_API int lvk_stage_connect(struct llama_context * ctx, const void * id, int n_stages, int stage);
-/* The same link through a host shared-memory ring (POSIX shm object `name`, opened by every
- * stage): any stage placement, several stages on one GPU included, no RCCL.  The call
- * returns once all n_stages stages have opened the ring. */
-/* 1 when this build carries the parked kernels (lib/dev: the persistent decode kernel,
- * the fused attention + Wo launch), 0 for the product library */
-LVK_API int lvk_dev_kernels(void);
+/* The same link through a host shared-memory ring (POSIX shm object `name`, a single path
+ * component such as "/lvk_run42"): any stage placement, several stages on one GPU included,
+ * no RCCL.  Stage 0 creates a fresh object under the name (removing one a crashed run left),
+ * the others wait for it; the call returns once all n_stages stages have joined, and stage 0
+ * then unlinks the name, so a reconnect (the only way on after an abort) under the same name
+ * starts clean.  Messages travel in 1 MiB pieces: the object takes
+ * n_stages * 4 MiB + 4 KiB of /dev/shm (32 MiB at 8 stages), reserved at connect -- a
+ * /dev/shm too small fails the connect with an error. */
 LVK_API int lvk_stage_connect_shm(struct llama_context * ctx, const char * name, int n_stages, int stage);
 LVK_API int lvk_stage_step(struct llama_context * ctx, const int * tokens, int n_tokens, int n_past, int greedy,
                            int micro);
+
+/* ggml_graph_compute keeps the host ranges of its tensors mirrored in HBM across calls and
+ * uploads only bytes a node reads before the call writes them, and of those only pages the
+ * host may have changed: pages of read-only mappings (a PROT_READ model file, an mprotect'ed
+ * buffer) while the mapping is unchanged, writable pages only where the kernel's soft-dirty
+ * bits track writes (else on every call).  Q4 weights are repacked once per upload.
+ * lvk_ggml_stats: the last call's out[0] host->device bytes, out[1] device->host bytes (the
+ * byte ranges the nodes wrote), out[2] bytes of Q4 weights repacked, out[3] host bytes
+ * mirrored in HBM after the call; out[4] the tracking mode (0 off: LVK_GGML_CACHE=0, 1
+ * read-only mappings only, 2 soft-dirty pages), out[5] 1 once any graph has run.  Fills
+ * min(n, 6) values, returns 6 (-1 on bad arguments).
+ * lvk_ggml_invalidate: the caller changed [p, p + n) in a way that tracking cannot see
+ * (write-enabled a read-only buffer, wrote, protected it again between two calls); its
+ * pages are uploaded again by the next call.  0 / -1. */
+LVK_API int lvk_ggml_stats(uint64_t * out, int n);
+LVK_API int lvk_ggml_invalidate(const void * p, size_t n);
+
+/* 1 when this build carries the parked kernels (lib/dev: the persistent decode kernel,
+ * the fused attention + Wo launch), 0 for the product library */
+LVK_API int lvk_dev_kernels(void);
 
 /* The layer split behind llama.h, one process driving n_stages HIP
  * devices: stage s holds layers [s*L/S, (s+1)*L/S) on devices[s].  llama_eval /

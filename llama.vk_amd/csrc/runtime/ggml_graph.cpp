@@ -10,7 +10,9 @@
 //     metadata only, as in ggml;
 //   * ggml_graph_compute mirrors every host buffer the graph touches into HBM, runs each
 //     node on the GPU in graph order (graph_ops.hip, the Q4 matvec kernels), and copies the
-//     node results back.  An operator without a GPU implementation aborts -- there is no
+//     bytes the nodes wrote back.  The mirrors, the repacked Q4 images and the temporaries'
+//     arena persist across calls: only host pages written since the previous call travel
+//     again (soft-dirty page tracking, below), so a caller's weights upload once.  An operator without a GPU implementation aborts -- there is no
 //     CPU fallback.
 #include <immintrin.h>
 
@@ -21,9 +23,15 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include "../../../include/ggml.h"
+#include "../../../include/lvk_ops.h"
 #include "lvk_context.h"
 
 namespace {
@@ -557,8 +565,14 @@ int ggml_cpu_has_avx(void) { return __builtin_cpu_supports("avx") ? 1 : 0; }
 int ggml_cpu_has_avx2(void) { return __builtin_cpu_supports("avx2") ? 1 : 0; }
 int ggml_cpu_has_avx512(void) { return __builtin_cpu_supports("avx512f") ? 1 : 0; }
 int ggml_cpu_has_fma(void) { return __builtin_cpu_supports("fma") ? 1 : 0; }
+int ggml_cpu_has_neon(void) { return 0; }
+int ggml_cpu_has_arm_fma(void) { return 0; }
 int ggml_cpu_has_f16c(void) { return 1; }
+int ggml_cpu_has_fp16_va(void) { return 0; }
+int ggml_cpu_has_wasm_simd(void) { return 0; }
 int ggml_cpu_has_blas(void) { return 0; }
+int ggml_cpu_has_sse3(void) { return __builtin_cpu_supports("sse3") ? 1 : 0; }
+int ggml_cpu_has_vsx(void) { return 0; }
 
 }  // extern "C"
 
@@ -578,43 +592,332 @@ size_t span_bytes(const ggml_tensor * t) {
     return s;
 }
 
-struct Region {
-    char * lo;
-    char * hi;
-    char * dev = nullptr;
-    bool written = false;
+// ---- host change tracking -------------------------------------------------------------
+// A graph's tensors live in caller memory that the caller may rewrite between calls (the next
+// token ids, a KV cache it restored ...), while most of it -- the weights -- never changes.
+// The mirrors below keep host ranges in HBM across calls and upload a page again only when
+// the host may have written it since it was uploaded:
+//   * pages inside a mapping this process cannot write (llama.cpp's PROT_READ model-file
+//     mapping, or a buffer the caller made read-only with mprotect) stay valid while that
+//     mapping (address range, offset, device, inode, permissions in /proc/self/maps) is
+//     unchanged -- a caller that re-enables writes, writes and protects again between two
+//     calls must say so with lvk_ggml_invalidate;
+//   * writable pages are tracked by the kernel's soft-dirty bits where they work
+//     (/proc/self/pagemap bit 55, cleared by "4" into /proc/self/clear_refs; a new mapping
+//     reads dirty, a page that is neither present nor swapped counts as written), and are
+//     uploaded again on every call where they do not;
+//   * only bytes a node reads before any node of the call writes them are uploaded at all
+//     (a node's output buffer never travels host -> device), and only the bytes the nodes
+//     wrote travel back.
+// LVK_GGML_CACHE=0 turns the caching off (every needed page uploaded on every call).
+constexpr size_t PAGE = 4096;
+
+struct MapEnt {
+    uintptr_t lo = 0, hi = 0;
+    uint64_t off = 0, inode = 0;
+    char perms[5] = {0};
+    char dev[16] = {0};
+    bool same(const MapEnt & o) const {
+        return lo == o.lo && hi == o.hi && off == o.off && inode == o.inode && !strcmp(perms, o.perms) &&
+               !strcmp(dev, o.dev);
+    }
 };
 
-// the device state of one ggml_graph_compute call
-struct GraphRun {
-    std::vector<Region> regions;
-    std::vector<void *> temps;
-    hipStream_t stream = nullptr;
-
-    ~GraphRun() {
-        if (stream) (void) hipStreamSynchronize(stream);
-        for (Region & r : regions)
-            if (r.dev) (void) hipFree(r.dev);
-        for (void * p : temps) (void) hipFree(p);
-        if (stream) (void) hipStreamDestroy(stream);
+std::vector<MapEnt> read_maps() {
+    std::vector<MapEnt> v;
+    FILE * f = fopen("/proc/self/maps", "r");
+    if (!f) return v;
+    char line[4096];
+    while (fgets(line, sizeof line, f)) {
+        MapEnt e;
+        unsigned long lo = 0, hi = 0, off = 0, ino = 0;
+        if (sscanf(line, "%lx-%lx %4s %lx %15s %lu", &lo, &hi, e.perms, &off, e.dev, &ino) < 6) continue;
+        e.lo = lo; e.hi = hi; e.off = off; e.inode = ino;
+        v.push_back(e);
     }
-    void * temp(size_t n) {
+    fclose(f);
+    return v;       // the kernel lists mappings in address order
+}
+
+const MapEnt * map_of(const std::vector<MapEnt> & v, uintptr_t a) {
+    auto it = std::upper_bound(v.begin(), v.end(), a, [](uintptr_t x, const MapEnt & e) { return x < e.lo; });
+    if (it == v.begin()) return nullptr;
+    --it;
+    return a < it->hi ? &*it : nullptr;
+}
+
+struct DirtyTracker {
+    int pagemap = -1, clear_refs = -1;
+    bool enabled = true;       // LVK_GGML_CACHE != 0
+    bool ok = false;           // soft-dirty bits work
+
+    bool read(uintptr_t page0, size_t n, std::vector<uint64_t> & e) const {
+        e.resize(n);
+        const size_t want = n * 8;
+        size_t got = 0;
+        while (got < want) {
+            const ssize_t r = pread(pagemap, (char *) e.data() + got, want - got, (off_t) (page0 * 8 + got));
+            if (r <= 0) return false;
+            got += (size_t) r;
+        }
+        return true;
+    }
+    static bool written(uint64_t e) {
+        const bool present = (e >> 63) & 1, swapped = (e >> 62) & 1, soft_dirty = (e >> 55) & 1;
+        return soft_dirty || (!present && !swapped);
+    }
+    bool clear() const { return pwrite(clear_refs, "4", 1, 0) == 1; }
+
+    DirtyTracker() {
+        const char * e = getenv("LVK_GGML_CACHE");
+        if (e && atoi(e) == 0) { enabled = false; return; }
+        pagemap = open("/proc/self/pagemap", O_RDONLY | O_CLOEXEC);
+        clear_refs = open("/proc/self/clear_refs", O_WRONLY | O_CLOEXEC);
+        if (pagemap < 0 || clear_refs < 0) return;
+        // self-test on a page of our own: written -> cleared -> written again
+        void * p = mmap(nullptr, PAGE, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) return;
+        volatile char * c = (volatile char *) p;
+        std::vector<uint64_t> v;
+        const uintptr_t pg = (uintptr_t) p / PAGE;
+        c[0] = 1;
+        bool good = clear() && read(pg, 1, v) && !written(v[0]);
+        c[1] = 2;
+        good = good && read(pg, 1, v) && written(v[0]);
+        munmap(p, PAGE);
+        ok = good;
+    }
+};
+
+DirtyTracker & tracker() {
+    static DirtyTracker t;
+    return t;
+}
+
+// a host range [lo, hi) mirrored in HBM; valid[i]: the bytes of host page (lo / PAGE + i)
+// inside the range equal the device copy
+struct Mirror {
+    char * lo = nullptr;
+    char * hi = nullptr;
+    char * dev = nullptr;
+    std::vector<uint8_t> valid;
+    std::vector<int32_t> ro;       // per page: the read-only mapping it was uploaded from, or -1
+    uint64_t last_call = 0;
+    uintptr_t page0() const { return (uintptr_t) lo / PAGE; }
+    size_t pages() const { return (uintptr_t) (hi - 1) / PAGE - page0() + 1; }
+};
+
+// a Q4 weight repacked into the decode kernels' octet image, keyed by its host address
+struct Repacked {
+    const char * lo;
+    const char * hi;
+    int qt, M, K;
+    uint4 * nib = nullptr;
+    void * scl = nullptr;
+};
+
+// grow-only device (or pinned host) arena, reset per call: no allocation per op
+struct Arena {
+    bool pinned = false;
+    std::vector<std::pair<char *, size_t>> chunks;
+    size_t cur = 0, off = 0;
+    void * get(size_t n) {
+        n = (n + 255) & ~(size_t) 255;
+        if (n == 0) n = 256;
+        while (cur < chunks.size()) {
+            if (off + n <= chunks[cur].second) {
+                void * p = chunks[cur].first + off;
+                off += n;
+                return p;
+            }
+            ++cur;
+            off = 0;
+        }
+        const size_t sz = std::max(n, chunks.empty() ? (size_t) 1 << 20 : chunks.back().second * 2);
         void * p = nullptr;
-        LVK_HIP(hipMalloc(&p, n ? n : 16));
-        temps.push_back(p);
+        if (pinned) LVK_HIP(hipHostMalloc(&p, sz, hipHostMallocDefault));
+        else LVK_HIP(hipMalloc(&p, sz));
+        chunks.push_back({(char *) p, sz});
+        cur = chunks.size() - 1;
+        off = n;
         return p;
     }
-    Region & region_of(const void * p) {
+    void reset() { cur = 0; off = 0; }
+};
+
+struct Span {
+    const char * lo;
+    const char * hi;
+};
+bool overlaps(const char * a0, const char * a1, const char * b0, const char * b1) { return a0 < b1 && b0 < a1; }
+
+struct GraphStats {
+    uint64_t h2d = 0, d2h = 0, repack = 0, mirrored = 0;
+};
+
+// the persistent device state of ggml_graph_compute on one device
+struct GraphEngine {
+    hipStream_t stream = nullptr;
+    std::vector<Mirror *> mirrors;          // sorted by lo, disjoint
+    std::vector<Repacked> repacked;
+    Arena dev_arena, host_arena;
+    uint64_t calls = 0;
+    GraphStats last;
+    // this call
+    std::vector<Mirror *> used;
+    std::vector<Span> written;              // node outputs of this call, in order
+
+    GraphEngine() {
+        host_arena.pinned = true;
+        LVK_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    }
+
+    Mirror & mirror_of(const void * p) {
         const char * c = (const char *) p;
-        auto it = std::upper_bound(regions.begin(), regions.end(), c, [](const char * v, const Region & r) { return v < r.lo; });
-        if (it == regions.begin()) gabort("ggml_graph_compute: tensor outside the mapped buffers");
-        --it;
-        if (c >= it->hi) gabort("ggml_graph_compute: tensor outside the mapped buffers");
-        return *it;
+        auto it = std::upper_bound(mirrors.begin(), mirrors.end(), c, [](const char * v, const Mirror * m) { return v < m->lo; });
+        if (it == mirrors.begin() || c >= (*(it - 1))->hi) gabort("ggml_graph_compute: tensor outside the mapped buffers");
+        return **(it - 1);
     }
     char * dev(const void * p) {
-        Region & r = region_of(p);
-        return r.dev + ((const char *) p - r.lo);
+        Mirror & m = mirror_of(p);
+        return m.dev + ((const char *) p - m.lo);
+    }
+    void * temp(size_t n) { return dev_arena.get(n); }
+    // host bytes that must reach the device in stream order: copied into pinned staging first,
+    // so the caller's memory may go away before the copy runs
+    void * upload_small(const void * src, size_t n) {
+        void * h = host_arena.get(n);
+        std::memcpy(h, src, n);
+        void * d = temp(n);
+        LVK_HIP(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, stream));
+        return d;
+    }
+    void drop_repacked(const char * lo, const char * hi) {
+        for (size_t i = 0; i < repacked.size();) {
+            if (overlaps(lo, hi, repacked[i].lo, repacked[i].hi)) {
+                (void) hipFree(repacked[i].nib);
+                (void) hipFree(repacked[i].scl);
+                repacked[i] = repacked.back();
+                repacked.pop_back();
+            } else {
+                ++i;
+            }
+        }
+    }
+
+    // one mirror covering [lo, hi): existing overlapping mirrors are merged into it (their
+    // device bytes copied over, their fully covered valid pages kept)
+    Mirror & ensure(char * lo, char * hi) {
+        std::vector<Mirror *> old;
+        for (Mirror * m : mirrors)
+            if (m->lo < hi && lo < m->hi) old.push_back(m);
+        if (old.size() == 1 && old[0]->lo <= lo && hi <= old[0]->hi) return *old[0];
+        Mirror * n = new Mirror;
+        n->lo = lo;
+        n->hi = hi;
+        for (Mirror * m : old) {
+            n->lo = std::min(n->lo, m->lo);
+            n->hi = std::max(n->hi, m->hi);
+        }
+        LVK_HIP(hipMalloc(&n->dev, (size_t) (n->hi - n->lo) + 16));
+        n->valid.assign(n->pages(), 0);
+        n->ro.assign(n->pages(), -1);
+        for (Mirror * m : old) {
+            LVK_HIP(hipMemcpyAsync(n->dev + (m->lo - n->lo), m->dev, (size_t) (m->hi - m->lo), hipMemcpyDeviceToDevice, stream));
+            const size_t np = m->pages(), d = m->page0() - n->page0();
+            for (size_t i = 0; i < np; ++i) {
+                // a page only partly inside the old range holds bytes the old mirror never had
+                const char * p0 = (const char *) ((m->page0() + i) * PAGE);
+                const bool whole = p0 >= m->lo && p0 + PAGE <= m->hi;
+                const bool edge_ok = (p0 < m->lo ? n->lo >= m->lo : true) && (p0 + PAGE > m->hi ? n->hi <= m->hi : true);
+                n->valid[d + i] = m->valid[i] && (whole || edge_ok);
+                n->ro[d + i] = m->ro[i];
+            }
+        }
+        LVK_HIP(hipStreamSynchronize(stream));
+        for (Mirror * m : old) {
+            (void) hipFree(m->dev);
+            mirrors.erase(std::find(mirrors.begin(), mirrors.end(), m));
+            delete m;
+        }
+        mirrors.insert(std::upper_bound(mirrors.begin(), mirrors.end(), n, [](const Mirror * a, const Mirror * b) { return a->lo < b->lo; }), n);
+        return *n;
+    }
+
+    // pages the host may have written since they were uploaded lose their validity
+    std::vector<MapEnt> ro_maps;           // identities of the read-only mappings pages came from
+    std::vector<uint8_t> ro_alive;         // this call: is ro_maps[i] still mapped, unchanged
+    std::vector<MapEnt> maps_now;          // /proc/self/maps of this call (no soft-dirty)
+    void snapshot_maps() {
+        maps_now = read_maps();
+        ro_alive.assign(ro_maps.size(), 0);
+        for (size_t i = 0; i < ro_maps.size(); ++i) {
+            const MapEnt * e = map_of(maps_now, ro_maps[i].lo);
+            ro_alive[i] = e && e->same(ro_maps[i]);
+        }
+    }
+    void refresh_validity(Mirror & m) {
+        DirtyTracker & T = tracker();
+        if (!T.enabled) { std::fill(m.valid.begin(), m.valid.end(), 0); return; }
+        if (T.ok) {
+            std::vector<uint64_t> e;
+            if (!T.read(m.page0(), m.pages(), e)) { std::fill(m.valid.begin(), m.valid.end(), 0); return; }
+            for (size_t i = 0; i < e.size(); ++i)
+                if (DirtyTracker::written(e[i])) m.valid[i] = 0;
+            return;
+        }
+        for (size_t i = 0; i < m.valid.size(); ++i)
+            if (m.ro[i] < 0 || !ro_alive[(size_t) m.ro[i]]) m.valid[i] = 0;
+    }
+    int32_t ro_id(uintptr_t page) {
+        const MapEnt * e = map_of(maps_now, page * PAGE);
+        if (!e || strchr(e->perms, 'w')) return -1;
+        for (size_t i = 0; i < ro_maps.size(); ++i)
+            if (ro_maps[i].same(*e)) return (int32_t) i;
+        ro_maps.push_back(*e);
+        ro_alive.push_back(1);
+        return (int32_t) ro_maps.size() - 1;
+    }
+
+    // the invalid pages of m that overlap [a, b) travel host -> device
+    void upload(Mirror & m, const char * a, const char * b) {
+        const size_t np = m.pages();
+        const size_t i0 = (uintptr_t) a / PAGE - m.page0(), i1 = std::min(np, (uintptr_t) (b - 1) / PAGE - m.page0() + 1);
+        const bool track_ro = tracker().enabled && !tracker().ok;
+        for (size_t i = i0; i < i1;) {
+            if (m.valid[i]) { ++i; continue; }
+            size_t j = i;
+            while (j < i1 && !m.valid[j]) ++j;
+            const char * x = std::max((const char *) ((m.page0() + i) * PAGE), (const char *) m.lo);
+            const char * y = std::min((const char *) ((m.page0() + j) * PAGE), (const char *) m.hi);
+            LVK_HIP(hipMemcpyAsync(m.dev + (x - m.lo), x, (size_t) (y - x), hipMemcpyHostToDevice, stream));
+            last.h2d += (uint64_t) (y - x);
+            drop_repacked(x, y);
+            for (size_t k = i; k < j; ++k) {
+                m.valid[k] = 1;
+                m.ro[k] = track_ro ? ro_id(m.page0() + k) : -1;
+            }
+            i = j;
+        }
+    }
+
+    // true when no node of this call has written [p, p + n) so far: the host bytes are current
+    bool host_current(const void * p, size_t n) const {
+        const char * a = (const char *) p;
+        for (const Span & w : written)
+            if (overlaps(a, a + n, w.lo, w.hi)) return false;
+        return true;
+    }
+    template <class T> T read_scalar(const ggml_tensor * t, int i) {
+        const char * p = (const char *) t->data + (size_t) i * sizeof(T);
+        T v;
+        if (host_current(p, sizeof(T))) {
+            std::memcpy(&v, p, sizeof(T));
+            return v;
+        }
+        LVK_HIP(hipMemcpyAsync(&v, dev(p), sizeof(T), hipMemcpyDeviceToHost, stream));
+        LVK_HIP(hipStreamSynchronize(stream));
+        return v;
     }
     lvk::GView view(const ggml_tensor * t) {
         lvk::GView v;
@@ -639,13 +942,43 @@ struct GraphRun {
         LVK_HIP(lvk::launch_g_cpy(view(t), d, stream));
         return p;
     }
-    template <class T> T read_scalar(const ggml_tensor * t, int i) {
-        T v;
-        LVK_HIP(hipMemcpyAsync(&v, dev((const char *) t->data + (size_t) i * sizeof(T)), sizeof(T), hipMemcpyDeviceToHost, stream));
-        LVK_HIP(hipStreamSynchronize(stream));
-        return v;
+    // the octet image of the Q4 matrix at host address w (M x K), repacked once and kept
+    // until the host bytes change
+    lvk::QMatrix qmatrix(const char * w, int qt, int M, int K) {
+        const char * hi = w + (size_t) M * (K / 32) * (qt == lvk::Q4_1 ? 24 : 20);
+        for (const Repacked & r : repacked)
+            if (r.lo == w && r.qt == qt && r.M == M && r.K == K) {
+                lvk::QMatrix q;
+                q.qtype = qt; q.M = M; q.K = K; q.nib = r.nib; q.scl = r.scl;
+                return q;
+            }
+        Repacked r{w, hi, qt, M, K};
+        LVK_HIP(hipMalloc(&r.nib, lvk::qimage_nib_bytes(M, K)));
+        LVK_HIP(hipMalloc(&r.scl, lvk::qimage_scl_bytes(M, K, qt)));
+        LVK_HIP(lvk::launch_repack(dev(w), qt, M, K, r.nib, r.scl, stream));
+        last.repack += (uint64_t) (hi - w);
+        repacked.push_back(r);
+        lvk::QMatrix q;
+        q.qtype = qt; q.M = M; q.K = K; q.nib = r.nib; q.scl = r.scl;
+        return q;
     }
 };
+
+// one engine per device, behind one lock (ggml contexts may be used from several threads)
+std::mutex & engine_mutex() {
+    static std::mutex m;
+    return m;
+}
+GraphEngine & engine() {
+    static std::map<int, GraphEngine *> per_dev;
+    int d = 0;
+    LVK_HIP(hipGetDevice(&d));
+    auto it = per_dev.find(d);
+    if (it != per_dev.end()) return *it->second;
+    return *per_dev.emplace(d, new GraphEngine).first->second;
+}
+GraphStats g_last_stats;
+bool g_have_engine = false;
 
 // fp16 exp / silu tables of this host's glibc (ggml.c:2915-2927) and the softmax exp mode,
 // once per device
@@ -671,7 +1004,7 @@ const Tables & tables() {
     return per_dev.emplace(dev, t).first->second;
 }
 
-void run_mul_mat_q(GraphRun & R, const ggml_tensor * a, const ggml_tensor * b, ggml_tensor * node) {
+void run_mul_mat_q(GraphEngine & R, const ggml_tensor * a, const ggml_tensor * b, ggml_tensor * node) {
     // ggml_compute_forward_mul_mat_q_f32 (ggml.c:6510-6696): every src1 row quantized with
     // the AVX2 quantizer, one vec_dot_q per (row, column) -- the matvec kernels' arithmetic
     const int M = (int) a->ne[1], K = (int) a->ne[0], N = (int) b->ne[1];
@@ -680,22 +1013,15 @@ void run_mul_mat_q(GraphRun & R, const ggml_tensor * a, const ggml_tensor * b, g
     G_ASSERT(a->nb[1] == (size_t) (K / 32) * TYPE_SIZE[a->type]);
     for (int64_t i3 = 0; i3 < a->ne[3]; ++i3)
         for (int64_t i2 = 0; i2 < a->ne[2]; ++i2) {
-            lvk::QMatrix q;
-            q.qtype = qt; q.M = M; q.K = K;
-            q.nib = (const uint4 *) R.temp(lvk::qimage_nib_bytes(M, K));
-            q.scl = R.temp(lvk::qimage_scl_bytes(M, K, qt));
-            const char * w = R.dev((const char *) a->data + i2 * a->nb[2] + i3 * a->nb[3]);
-            LVK_HIP(lvk::launch_repack(w, qt, M, K, (uint4 *) q.nib, (void *) q.scl, R.stream));
+            const lvk::QMatrix q = R.qmatrix((const char *) a->data + i2 * a->nb[2] + i3 * a->nb[3], qt, M, K);
             // this batch's src1 rows, contiguous
             ggml_tensor bs = *b;
             bs.data = (char *) b->data + i2 * b->nb[2] + i3 * b->nb[3];
             bs.ne[2] = bs.ne[3] = 1;
             float * x = (float *) R.gather(&bs, lvk::GT_F32);
             float * y = (float *) R.temp((size_t) N * M * 4);
-            lvk::StepParams sp{0, N, 0, 0};
-            lvk::StepParams * spd = (lvk::StepParams *) R.temp(sizeof sp);
-            LVK_HIP(hipMemcpyAsync(spd, &sp, sizeof sp, hipMemcpyHostToDevice, R.stream));
-            LVK_HIP(hipStreamSynchronize(R.stream));      // sp is this scope's host memory
+            const lvk::StepParams sp{0, N, 0, 0};
+            lvk::StepParams * spd = (lvk::StepParams *) R.upload_small(&sp, sizeof sp);
             lvk::MvLaunch L;
             L.w = q; L.sp = spd; L.n_tokens = N; L.y = y;
             if (qt == lvk::Q4_1) {
@@ -723,7 +1049,7 @@ void run_mul_mat_q(GraphRun & R, const ggml_tensor * a, const ggml_tensor * b, g
         }
 }
 
-void run_node(GraphRun & R, ggml_tensor * n) {
+void run_node(GraphEngine & R, ggml_tensor * n) {
     ggml_tensor * a = n->src0;
     ggml_tensor * b = n->src1;
     switch (n->op) {
@@ -797,17 +1123,15 @@ void run_node(GraphRun & R, ggml_tensor * n) {
                     cs[(size_t) t * (n_dims / 2) + i0 / 2] = make_float2(cosf(ang), sinf(ang));
                 }
             }
-            float2 * csd = (float2 *) R.temp(cs.size() * sizeof(float2));
-            LVK_HIP(hipMemcpyAsync(csd, cs.data(), cs.size() * sizeof(float2), hipMemcpyHostToDevice, R.stream));
+            const float2 * csd = (const float2 *) R.upload_small(cs.data(), cs.size() * sizeof(float2));
             LVK_HIP(lvk::launch_g_rope(R.view(n), R.view(n), csd, n_dims, i2_0, R.stream));
-            LVK_HIP(hipStreamSynchronize(R.stream));     // cs is host memory of this scope
             return;
         }
         case GGML_OP_GET_ROWS:
             G_ASSERT(b->type == GGML_TYPE_I32 && n->type == GGML_TYPE_F32);
             G_ASSERT(a->type == GGML_TYPE_Q4_0 || a->type == GGML_TYPE_Q4_1 || a->type == GGML_TYPE_F16 ||
                      a->type == GGML_TYPE_F32);
-            if (b->op == GGML_OP_NONE)
+            if (b->op == GGML_OP_NONE && R.host_current(b->data, (size_t) b->ne[0] * sizeof(int32_t)))
                 for (int64_t i = 0; i < b->ne[0]; ++i) {
                     const int32_t id = ((const int32_t *) b->data)[i];
                     if (id < 0 || id >= a->ne[1]) gabort("ggml_get_rows: row index out of range");
@@ -835,12 +1159,25 @@ void run_node(GraphRun & R, ggml_tensor * n) {
     }
 }
 
+// the ops that only reinterpret their source: they write nothing
+bool writes_data(int op) {
+    return op != GGML_OP_NONE && op != GGML_OP_RESHAPE && op != GGML_OP_VIEW && op != GGML_OP_PERMUTE &&
+           op != GGML_OP_TRANSPOSE;
+}
+
 }  // namespace
 
 extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph * cgraph) {
     (void) ctx;
+    std::lock_guard<std::mutex> lock(engine_mutex());
     try {
-        GraphRun R;
+        GraphEngine & R = engine();
+        R.last = GraphStats{};
+        R.used.clear();
+        R.written.clear();
+        R.dev_arena.reset();
+        R.host_arena.reset();
+        ++R.calls;
         // every buffer range the graph reads or writes, merged into regions
         std::vector<const ggml_tensor *> ts;
         auto add = [&](const ggml_tensor * t) {
@@ -856,24 +1193,66 @@ extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph
             add(n->src1);
             for (int k = 0; k < GGML_MAX_OPT; ++k) add(n->opt[k]);
         }
-        std::vector<Region> sp;
-        for (const ggml_tensor * t : ts) sp.push_back({(char *) t->data, (char *) t->data + span_bytes(t)});
-        std::sort(sp.begin(), sp.end(), [](const Region & x, const Region & y) { return x.lo < y.lo; });
-        for (const Region & r : sp) {
-            if (!R.regions.empty() && r.lo <= R.regions.back().hi) R.regions.back().hi = std::max(R.regions.back().hi, r.hi);
-            else R.regions.push_back(r);
+        std::vector<Span> sp;
+        for (const ggml_tensor * t : ts) sp.push_back({(const char *) t->data, (const char *) t->data + span_bytes(t)});
+        std::sort(sp.begin(), sp.end(), [](const Span & x, const Span & y) { return x.lo < y.lo; });
+        std::vector<Span> regions;
+        for (const Span & r : sp) {
+            if (!regions.empty() && r.lo <= regions.back().hi) regions.back().hi = std::max(regions.back().hi, r.hi);
+            else regions.push_back(r);
         }
-        LVK_HIP(hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking));
-        for (Region & r : R.regions) {
-            LVK_HIP(hipMalloc(&r.dev, (size_t) (r.hi - r.lo) + 16));
-            LVK_HIP(hipMemcpyAsync(r.dev, r.lo, (size_t) (r.hi - r.lo), hipMemcpyHostToDevice, R.stream));
+        // mirrors: created or merged
+        for (const Span & r : regions) {
+            Mirror & m = R.ensure((char *) r.lo, (char *) r.hi);
+            if (m.last_call != R.calls) {
+                m.last_call = R.calls;
+                R.used.push_back(&m);
+            }
+        }
+        DirtyTracker & T = tracker();
+        if (T.enabled && !T.ok) R.snapshot_maps();
+        for (Mirror * m : R.used) R.refresh_validity(*m);
+        // the bytes a node reads before any earlier node of this call wrote them (leaves, the
+        // caller's inputs, a KV cache) are the only ones that must come from the host
+        {
+            std::vector<Span> wr;          // written so far (unsorted; graphs are small)
+            std::vector<Span> need;
+            auto read_of = [&](const ggml_tensor * t) {
+                if (!t) return;
+                Span s{(const char *) t->data, (const char *) t->data + span_bytes(t)};
+                // subtract the written spans from s
+                std::vector<Span> parts{s};
+                for (const Span & w : wr) {
+                    std::vector<Span> next;
+                    for (const Span & p : parts) {
+                        if (!overlaps(p.lo, p.hi, w.lo, w.hi)) { next.push_back(p); continue; }
+                        if (p.lo < w.lo) next.push_back({p.lo, w.lo});
+                        if (w.hi < p.hi) next.push_back({w.hi, p.hi});
+                    }
+                    parts.swap(next);
+                    if (parts.empty()) break;
+                }
+                need.insert(need.end(), parts.begin(), parts.end());
+            };
+            for (int i = 0; i < cgraph->n_nodes; ++i) {
+                const ggml_tensor * n = cgraph->nodes[i];
+                read_of(n->src0);
+                read_of(n->src1);
+                for (int k = 0; k < GGML_MAX_OPT; ++k) read_of(n->opt[k]);
+                if (writes_data(n->op)) wr.push_back({(const char *) n->data, (const char *) n->data + span_bytes(n)});
+            }
+            for (const Span & p : need) R.upload(R.mirror_of(p.lo), p.lo, p.hi);
         }
         // LVK_GGML_SYNC=1: wait for every node and name the one that fails (debugging)
         static const bool sync_each = getenv("LVK_GGML_SYNC") && atoi(getenv("LVK_GGML_SYNC")) != 0;
         for (int i = 0; i < cgraph->n_nodes; ++i) {
             ggml_tensor * n = cgraph->nodes[i];
             run_node(R, n);
-            if (n->op != GGML_OP_NONE) R.region_of(n->data).written = true;
+            if (writes_data(n->op)) {
+                const Span w{(const char *) n->data, (const char *) n->data + span_bytes(n)};
+                R.written.push_back(w);
+                R.drop_repacked(w.lo, w.hi);
+            }
             if (sync_each) {
                 const hipError_t e = hipStreamSynchronize(R.stream);
                 if (e != hipSuccess) {
@@ -884,11 +1263,76 @@ extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph
                 }
             }
         }
-        for (Region & r : R.regions)
-            if (r.written) LVK_HIP(hipMemcpyAsync(r.lo, r.dev, (size_t) (r.hi - r.lo), hipMemcpyDeviceToHost, R.stream));
+        // node results back to the host: the written byte ranges only (merged)
+        std::vector<Span> wb = R.written;
+        std::sort(wb.begin(), wb.end(), [](const Span & x, const Span & y) { return x.lo < y.lo; });
+        std::vector<Span> wm;
+        for (const Span & w : wb) {
+            if (!wm.empty() && w.lo <= wm.back().hi) wm.back().hi = std::max(wm.back().hi, w.hi);
+            else wm.push_back(w);
+        }
+        for (const Span & w : wm) {
+            LVK_HIP(hipMemcpyAsync((void *) w.lo, R.dev(w.lo), (size_t) (w.hi - w.lo), hipMemcpyDeviceToHost, R.stream));
+            R.last.d2h += (uint64_t) (w.hi - w.lo);
+        }
         LVK_HIP(hipStreamSynchronize(R.stream));
+        // mirrors this call did not use: note their host writes before the bits are cleared;
+        // mirrors unused for 8 calls are freed (a caller's per-call scratch contexts)
+        for (size_t i = 0; i < R.mirrors.size();) {
+            Mirror * m = R.mirrors[i];
+            if (m->last_call + 8 < R.calls) {
+                R.drop_repacked(m->lo, m->hi);
+                (void) hipFree(m->dev);
+                R.mirrors.erase(R.mirrors.begin() + (long) i);
+                delete m;
+                continue;
+            }
+            if (m->last_call != R.calls && T.ok) R.refresh_validity(*m);
+            ++i;
+        }
+        if (T.ok && !T.clear()) {
+            T.ok = false;
+            for (Mirror * m : R.mirrors) std::fill(m->valid.begin(), m->valid.end(), 0);
+        }
+        uint64_t resident = 0;
+        for (Mirror * m : R.mirrors) resident += (uint64_t) (m->hi - m->lo);
+        R.last.mirrored = resident;
+        g_last_stats = R.last;
+        g_have_engine = true;
         cgraph->perf_runs++;
     } catch (const lvk::Error & e) {
         gabort(e.msg.c_str());
     }
+}
+
+extern "C" int lvk_ggml_stats(uint64_t * out, int n) {
+    std::lock_guard<std::mutex> lock(engine_mutex());
+    const DirtyTracker & T = tracker();
+    const uint64_t v[6] = {g_last_stats.h2d, g_last_stats.d2h, g_last_stats.repack, g_last_stats.mirrored,
+                           (uint64_t) (!T.enabled ? 0 : T.ok ? 2 : 1), (uint64_t) (g_have_engine ? 1 : 0)};
+    if (!out || n < 0) return -1;
+    for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
+    return 6;
+}
+
+// the caller rewrote [p, p + n) in a way the tracking cannot see (see above): upload it again
+extern "C" int lvk_ggml_invalidate(const void * p, size_t n) {
+    std::lock_guard<std::mutex> lock(engine_mutex());
+    if (!p) return -1;
+    try {
+        GraphEngine & R = engine();
+        const char * a = (const char *) p;
+        const char * b = a + n;
+        for (Mirror * m : R.mirrors) {
+            if (!overlaps(a, b, m->lo, m->hi)) continue;
+            const size_t i0 = (uintptr_t) std::max(a, (const char *) m->lo) / PAGE - m->page0();
+            const size_t i1 = (uintptr_t) (std::min(b, (const char *) m->hi) - 1) / PAGE - m->page0() + 1;
+            for (size_t i = i0; i < i1; ++i) m->valid[i] = 0;
+        }
+        R.drop_repacked(a, b);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "lvk_ggml_invalidate: %s\n", e.msg.c_str());
+        return -1;
+    }
+    return 0;
 }

@@ -426,6 +426,7 @@ int lvk_stage_connect(struct llama_context * ctx, const void * id, int n_stages,
     try {
         check_stage_position(ctx, n_stages, stage);
         if (!id) throw lvk::Error("bad stage link arguments");
+        ctx->c.link.reset();             // an earlier link of this context (aborted or not) goes first
         std::unique_ptr<lvk::StageLink, lvk::StageLinkDel> L(new lvk::StageLink);
         L->stage = stage;
         L->n_stages = n_stages;
@@ -443,10 +444,11 @@ int lvk_stage_connect_shm(struct llama_context * ctx, const char * name, int n_s
         check_stage_position(ctx, n_stages, stage);
         if (!name || !name[0]) throw lvk::Error("bad stage link arguments");
         lvk::Context & c = ctx->c;
+        c.link.reset();                  // an earlier link of this context (aborted or not) goes first
         std::unique_ptr<lvk::StageLink, lvk::StageLinkDel> L(new lvk::StageLink);
         L->stage = stage;
         L->n_stages = n_stages;
-        L->t = lvk::make_shm_transport(name, n_stages, stage, (size_t) c.n_ctx * c.model.hp.n_embd * sizeof(float));
+        L->t = lvk::make_shm_transport(name, n_stages, stage);
         c.link = std::move(L);
     } catch (const lvk::Error & e) {
         fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());

@@ -125,6 +125,8 @@ void Context::init(const llama_context_params & p) {
         LVK_HIP(hipMemset(attn_gran, 0, attention_decode_scratch_bytes((int) H, (int) C)));
         // granule tags (seq << 7) + layer + 1 stay unique per token with up to 126 layers
         seq_epochs = !fuse_attn_wo && L <= 126;
+        // test hook (tests/test_gpu_seq_wrap.py): start the step counter near its 25-bit wrap
+        if (const char * e = getenv("LVK_SEQ_START")) seq = (unsigned) strtoul(e, nullptr, 0) & ((1u << 25) - 1);
     }
     {
         // persistent decode state: the layer table and the in-launch exchange buffers

@@ -7,6 +7,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -286,20 +288,34 @@ struct RcclTransport final : StageTransport {
 
 // Host shared-memory ring (POSIX shm, every stage opens the same name): ring s carries
 // stage s -> (s + 1) % S, so ring S-1 is the greedy relay from the last stage to the first.
+// A message larger than a slot travels as consecutive slot-sized pieces, so the object's
+// size does not grow with n_ctx (S * SHM_SLOTS * SHM_SLOT_BYTES + 4 KiB: 32 MiB at S = 8).
 // The sender waits for its stream and copies the device buffer into the next free slot,
 // then publishes it; the receiver copies the slot into its device buffer on its stream and
 // frees the slot.  One abort word fails every stage's waits.
-constexpr int SHM_SLOTS = 2;
+//
+// Life cycle: stage 0 removes any object left under the name (a crashed run), creates a
+// fresh one (O_EXCL), reserves its pages (posix_fallocate: a /dev/shm too small fails here
+// with an error instead of SIGBUS on the first write), writes the header and only then the
+// magic word.  The other stages open the name, wait for the magic, check n_stages and the
+// slot size, and join.  Once all S have joined, stage 0 unlinks the name: the mappings stay
+// valid, nothing is left in /dev/shm, and a reconnect under the same name starts from a new
+// zeroed object.  A stage that mapped a stale object (the name was replaced under it) sees
+// the inode change while it waits and reopens.
+constexpr int SHM_SLOTS = 4;
+constexpr size_t SHM_SLOT_BYTES = (size_t) 1 << 20;
+constexpr uint64_t SHM_MAGIC = 0x6c766b73686d3031ull;   // "lvkshm01"
 struct ShmRing {
-    std::atomic<uint64_t> head;        // messages published (the sender writes)
-    std::atomic<uint64_t> tail;        // messages consumed (the receiver writes)
+    std::atomic<uint64_t> head;        // pieces published (the sender writes)
+    std::atomic<uint64_t> tail;        // pieces consumed (the receiver writes)
     uint64_t bytes[SHM_SLOTS];
 };
 struct ShmHeader {
+    std::atomic<uint64_t> magic;       // SHM_MAGIC once stage 0 has initialised the object
     std::atomic<uint32_t> abort;
     std::atomic<uint32_t> joined;
     uint32_t n_stages;
-    uint32_t pad;
+    uint32_t slots;
     uint64_t slot_bytes;
 };
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory rings need address-free atomics");
@@ -308,9 +324,10 @@ constexpr size_t SHM_DATA_OFF = 4096;
 struct ShmTransport final : StageTransport {
     std::string shm_name;
     int S = 1, stage = 0;
-    size_t slot = 0, total = 0;
+    size_t slot = SHM_SLOT_BYTES, total = 0;
     uint8_t * base = nullptr;
     ShmHeader * h = nullptr;
+    bool named = false;                // stage 0: the name still points at our object
     const char * name() const override { return "shm"; }
     ShmRing * ring(int r) const { return (ShmRing *) (base + sizeof(ShmHeader)) + r; }
     uint8_t * data(int r, uint64_t seq) const {
@@ -330,56 +347,134 @@ struct ShmTransport final : StageTransport {
             if (i > 1024) std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
     }
-    void open_ring(const char * nm, int n_stages, int st, size_t slot_bytes) {
-        shm_name = nm[0] == '/' ? nm : std::string("/") + nm;
-        S = n_stages;
-        stage = st;
-        slot = (slot_bytes + 4095) & ~(size_t) 4095;
-        total = SHM_DATA_OFF + (size_t) S * SHM_SLOTS * slot;
-        if (sizeof(ShmHeader) + (size_t) S * sizeof(ShmRing) > SHM_DATA_OFF) throw Error("llama.vk_amd: too many stages for the shm link");
-        const int fd = shm_open(shm_name.c_str(), O_CREAT | O_RDWR, 0600);
-        if (fd < 0) throw Error("llama.vk_amd: shm_open(" + shm_name + ") failed: " + strerror(errno));
-        // every stage sizes the object alike; a fresh object reads as zeros
-        if (ftruncate(fd, (off_t) total) != 0) {
-            const int e = errno;
+    void unmap() {
+        if (base) munmap(base, total);
+        base = nullptr;
+        h = nullptr;
+    }
+    // stage 0: a fresh object under the name, header written, magic last
+    void create() {
+        shm_unlink(shm_name.c_str());               // a stale object of a crashed run (ENOENT is fine)
+        const int fd = shm_open(shm_name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0) throw Error("llama.vk_amd: shm_open(" + shm_name + ", O_EXCL) failed: " + strerror(errno));
+        named = true;
+        int e = ftruncate(fd, (off_t) total) == 0 ? 0 : errno;
+        if (!e) e = posix_fallocate(fd, 0, (off_t) total);
+        if (e) {
             close(fd);
-            throw Error("llama.vk_amd: ftruncate(" + shm_name + ") failed: " + strerror(e));
+            shm_unlink(shm_name.c_str());
+            named = false;
+            throw Error("llama.vk_amd: the shm link needs " + std::to_string(total >> 20) + " MiB in /dev/shm (" +
+                        shm_name + "): " + strerror(e));
         }
         void * p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         close(fd);
         if (p == MAP_FAILED) throw Error("llama.vk_amd: mmap of the shm link failed");
         base = (uint8_t *) p;
         h = (ShmHeader *) base;
-        // every stage must map the same object before any of them may unlink it
-        h->joined.fetch_add(1, std::memory_order_acq_rel);
-        spin_until([&] { return h->joined.load(std::memory_order_acquire) >= (uint32_t) S; }, "joining");
+        h->n_stages = (uint32_t) S;
+        h->slots = SHM_SLOTS;
+        h->slot_bytes = slot;
+        h->joined.store(0, std::memory_order_relaxed);
+        h->abort.store(0, std::memory_order_relaxed);
+        h->magic.store(SHM_MAGIC, std::memory_order_release);
+    }
+    // stages 1..S-1: map the object once it exists and is initialised; false = try again
+    bool try_open(ino_t & ino) {
+        const int fd = shm_open(shm_name.c_str(), O_RDWR, 0600);
+        if (fd < 0) return false;
+        struct stat sb;
+        if (fstat(fd, &sb) != 0 || (size_t) sb.st_size < total) { close(fd); return false; }
+        void * p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (p == MAP_FAILED) return false;
+        base = (uint8_t *) p;
+        h = (ShmHeader *) base;
+        if (h->magic.load(std::memory_order_acquire) != SHM_MAGIC) { unmap(); return false; }
+        if (h->n_stages != (uint32_t) S || h->slots != (uint32_t) SHM_SLOTS || h->slot_bytes != slot) {
+            unmap();
+            throw Error("llama.vk_amd: shm link " + shm_name + " was created for another stage count or slot size");
+        }
+        ino = sb.st_ino;
+        return true;
+    }
+    // the name now refers to another object (or none) and ours was not completed: stale
+    bool replaced(ino_t ino) const {
+        struct stat sb;
+        const std::string path = "/dev/shm" + shm_name;
+        return stat(path.c_str(), &sb) == 0 && sb.st_ino != ino;
+    }
+    void open_ring(const char * nm, int n_stages, int st) {
+        shm_name = nm[0] == '/' ? nm : std::string("/") + nm;
+        if (shm_name.find('/', 1) != std::string::npos) throw Error("llama.vk_amd: shm link names may not contain '/'");
+        S = n_stages;
+        stage = st;
+        total = SHM_DATA_OFF + (size_t) S * SHM_SLOTS * slot;
+        if (sizeof(ShmHeader) + (size_t) S * sizeof(ShmRing) > SHM_DATA_OFF) throw Error("llama.vk_amd: too many stages for the shm link");
+        const double limit = stage_timeout_s();
+        const auto t0 = Clock::now();
+        if (stage == 0) {
+            create();
+            h->joined.fetch_add(1, std::memory_order_acq_rel);
+            spin_until([&] { return h->joined.load(std::memory_order_acquire) >= (uint32_t) S; }, "joining");
+            shm_unlink(shm_name.c_str());             // every stage has mapped it
+            named = false;
+            return;
+        }
+        for (int i = 0;; ++i) {
+            ino_t ino = 0;
+            if (try_open(ino)) {
+                h->joined.fetch_add(1, std::memory_order_acq_rel);
+                bool stale = false;
+                for (int k = 0; h->joined.load(std::memory_order_acquire) < (uint32_t) S; ++k) {
+                    if (h->abort.load(std::memory_order_acquire)) throw Error("llama.vk_amd: stage link aborted by a peer (joining)");
+                    if (since_s(t0) > limit) { abort(); throw Error("llama.vk_amd: stage link timed out (joining)"); }
+                    if ((k & 255) == 255 && replaced(ino)) { stale = true; break; }
+                    if (k > 1024) std::this_thread::sleep_for(std::chrono::microseconds(50));
+                }
+                if (!stale) return;
+                unmap();
+            }
+            if (since_s(t0) > limit) throw Error("llama.vk_amd: stage link timed out waiting for stage 0 to create " + shm_name);
+            std::this_thread::sleep_for(std::chrono::microseconds(i < 100 ? 100 : 1000));
+        }
     }
     ~ShmTransport() override {
-        if (base) munmap(base, total);
-        if (stage == 0 && !shm_name.empty()) shm_unlink(shm_name.c_str());
+        unmap();
+        if (named) shm_unlink(shm_name.c_str());       // stage 0 failed before every stage joined
     }
     void send(const void * d, size_t bytes, int peer, hipStream_t s) override {
-        if (peer != (stage + 1) % S || bytes > slot) throw Error("llama.vk_amd: bad shm link send");
+        if (peer != (stage + 1) % S) throw Error("llama.vk_amd: bad shm link send");
         ShmRing & r = *ring(stage);
-        const uint64_t seq = r.head.load(std::memory_order_relaxed);
         LVK_HIP(hipStreamSynchronize(s));
-        spin_until([&] { return seq - r.tail.load(std::memory_order_acquire) < (uint64_t) SHM_SLOTS; }, "free slot");
-        LVK_HIP(hipMemcpy(data(stage, seq), d, bytes, hipMemcpyDeviceToHost));
-        r.bytes[seq % SHM_SLOTS] = bytes;
-        r.head.store(seq + 1, std::memory_order_release);
+        size_t off = 0;
+        do {
+            const size_t n = std::min(slot, bytes - off);
+            const uint64_t seq = r.head.load(std::memory_order_relaxed);
+            spin_until([&] { return seq - r.tail.load(std::memory_order_acquire) < (uint64_t) SHM_SLOTS; }, "free slot");
+            LVK_HIP(hipMemcpy(data(stage, seq), (const uint8_t *) d + off, n, hipMemcpyDeviceToHost));
+            r.bytes[seq % SHM_SLOTS] = n;
+            r.head.store(seq + 1, std::memory_order_release);
+            off += n;
+        } while (off < bytes);
     }
     void recv(void * d, size_t bytes, int peer, hipStream_t s) override {
-        if (peer != (stage + S - 1) % S || bytes > slot) throw Error("llama.vk_amd: bad shm link recv");
+        if (peer != (stage + S - 1) % S) throw Error("llama.vk_amd: bad shm link recv");
         ShmRing & r = *ring(peer);
-        const uint64_t seq = r.tail.load(std::memory_order_relaxed);
-        spin_until([&] { return r.head.load(std::memory_order_acquire) > seq; }, "message");
-        if (r.bytes[seq % SHM_SLOTS] != bytes) {
-            abort();
-            throw Error("llama.vk_amd: shm link message size differs between neighbouring stages");
-        }
-        LVK_HIP(hipMemcpyAsync(d, data(peer, seq), bytes, hipMemcpyHostToDevice, s));
-        LVK_HIP(hipStreamSynchronize(s));     // the slot is reused once tail moves
-        r.tail.store(seq + 1, std::memory_order_release);
+        size_t off = 0;
+        do {
+            const size_t n = std::min(slot, bytes - off);
+            const uint64_t seq = r.tail.load(std::memory_order_relaxed);
+            spin_until([&] { return r.head.load(std::memory_order_acquire) > seq; }, "message");
+            if (r.bytes[seq % SHM_SLOTS] != n) {
+                abort();
+                throw Error("llama.vk_amd: shm link message size differs between neighbouring stages");
+            }
+            LVK_HIP(hipMemcpyAsync((uint8_t *) d + off, data(peer, seq), n, hipMemcpyHostToDevice, s));
+            LVK_HIP(hipStreamSynchronize(s));     // the slot is reused once tail moves
+            r.tail.store(seq + 1, std::memory_order_release);
+            off += n;
+        } while (off < bytes);
     }
     void wait(hipStream_t s) override { LVK_HIP(hipStreamSynchronize(s)); }
     void abort() noexcept override {
@@ -399,9 +494,9 @@ std::unique_ptr<StageTransport> make_rccl_transport(const void * unique_id, int 
     return t;
 }
 
-std::unique_ptr<StageTransport> make_shm_transport(const char * name, int n_stages, int stage, size_t slot_bytes) {
+std::unique_ptr<StageTransport> make_shm_transport(const char * name, int n_stages, int stage) {
     std::unique_ptr<ShmTransport> t(new ShmTransport);
-    t->open_ring(name, n_stages, stage, slot_bytes);
+    t->open_ring(name, n_stages, stage);
     return t;
 }
 

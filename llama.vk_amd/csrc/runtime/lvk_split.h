@@ -102,9 +102,10 @@ struct StageLink {
 
 // one RCCL communicator of S ranks (one GPU each)
 std::unique_ptr<StageTransport> make_rccl_transport(const void * unique_id, int n_stages, int stage, int device);
-// a POSIX shared-memory ring named `name` (every stage opens the same name); slot_bytes is
-// the largest message (n_ctx * n_embd * 4)
-std::unique_ptr<StageTransport> make_shm_transport(const char * name, int n_stages, int stage, size_t slot_bytes);
+// a POSIX shared-memory ring named `name` (every stage opens the same name; stage 0 creates
+// it and unlinks the name once all stages have joined); messages of any size travel in
+// 1 MiB pieces
+std::unique_ptr<StageTransport> make_shm_transport(const char * name, int n_stages, int stage);
 // seconds a stage step may wait on its link (LVK_STAGE_TIMEOUT_S, default 300)
 double stage_timeout_s();
 

@@ -7,12 +7,14 @@
 // ggjt v1 with 32-byte aligned data, hparams ftype = itype.
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include <immintrin.h>
 
+#include "../../../include/ggml.h"
 #include "../../../include/llama.h"
 
 namespace {
@@ -37,10 +39,15 @@ void put(std::vector<uint8_t> & o, const void * p, size_t n) {
 }
 void put_u32(std::vector<uint8_t> & o, uint32_t v) { put(o, &v, 4); }
 
+// quantize_row_q4_0_reference (ggml.c:509-543).  MAX(a, b) is ((a) > (b) ? (a) : (b)): a NaN
+// input makes amax NaN, exactly as in the reference
 void quant_q4_0(const float * x, uint8_t * y, int k) {
     for (int i = 0; i < k / 32; ++i) {
         float amax = 0.0f;
-        for (int l = 0; l < 32; ++l) amax = std::max(amax, std::fabs(x[i * 32 + l]));
+        for (int l = 0; l < 32; ++l) {
+            const float a = std::fabs(x[i * 32 + l]);
+            amax = amax > a ? amax : a;
+        }
         const float d = amax / 7.0f;
         const float id = d != 0.0f ? 1.0f / d : 0.0f;
         uint8_t * blk = y + (size_t) i * 20;
@@ -53,6 +60,7 @@ void quant_q4_0(const float * x, uint8_t * y, int k) {
     }
 }
 
+// quantize_row_q4_1_reference (ggml.c:799-838)
 void quant_q4_1(const float * x, uint8_t * y, int k) {
     for (int i = 0; i < k / 32; ++i) {
         float mn = 3.402823466e+38f, mx = -3.402823466e+38f;
@@ -72,6 +80,28 @@ void quant_q4_1(const float * x, uint8_t * y, int k) {
             blk[8 + l / 2] = (uint8_t) (a | (b << 4));
         }
     }
+}
+
+// ggml_quantize_q4_0/_q4_1 (ggml.c:10520-10564): rows of k, then the nibble histogram
+size_t quantize_hist(const float * src, void * dst, int n, int k, int64_t * hist, bool q41) {
+    if (k <= 0 || k % 32 != 0 || n < 0) {
+        fprintf(stderr, "ggml_quantize_q4_%d: k must be a positive multiple of 32\n", q41 ? 1 : 0);
+        abort();
+    }
+    const size_t bs = q41 ? 24 : 20, off = q41 ? 8 : 4;
+    const int nb = k / 32;
+    for (int j = 0; j < n; j += k) {
+        uint8_t * y = (uint8_t *) dst + (size_t) (j / 32) * bs;
+        if (q41) quant_q4_1(src + j, y, k);
+        else quant_q4_0(src + j, y, k);
+        for (int i = 0; i < nb; ++i)
+            for (int l = 0; l < 16; ++l) {
+                const uint8_t q = y[(size_t) i * bs + off + l];
+                hist[q & 0xF]++;
+                hist[q >> 4]++;
+            }
+    }
+    return (size_t) (n / 32) * bs;
 }
 
 size_t row_bytes(uint32_t t, size_t k) {
@@ -166,6 +196,14 @@ void quantize_file(const char * fin, const char * fout, int itype) {
 }
 
 }  // namespace
+
+extern "C" size_t ggml_quantize_q4_0(const float * src, void * dst, int n, int k, int64_t * hist) {
+    return quantize_hist(src, dst, n, k, hist, false);
+}
+
+extern "C" size_t ggml_quantize_q4_1(const float * src, void * dst, int n, int k, int64_t * hist) {
+    return quantize_hist(src, dst, n, k, hist, true);
+}
 
 extern "C" int llama_model_quantize(const char * fname_inp, const char * fname_out, int itype) {
     try {

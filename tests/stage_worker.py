@@ -7,6 +7,8 @@ usage: stage_worker.py <model> <n_stages> <stage> <shm name> <mode> <out.npz> [n
                   prompt logits, every greedy token is saved by stages 0 and S-1
   mode badtoken : like run, but stage 0 passes an out-of-range token at greedy step 3;
                   every stage must fail that step (none may hang)
+  mode reconnect: like badtoken, then every stage reconnects under the same shm name and
+                  redoes step 3 with the right token: the stream must be run's
 No torch in this process (lvk.py refuses to share a process with torch's HIP runtime).
 """
 import os
@@ -38,13 +40,16 @@ def main():
     t0 = time.time()
     for i in range(10):
         arg = tok
-        if mode == "badtoken" and first and i == 3:
+        if mode in ("badtoken", "reconnect") and first and i == 3:
             arg = hp["n_vocab"] + 5
         try:
             tok = st.stage_step([arg] if first else None, 1, len(PROMPT) + i, greedy=True)
         except RuntimeError:
             failed_at = i
-            break
+            if mode != "reconnect":
+                break
+            st.stage_connect_shm(name, S, s)
+            tok = st.stage_step([tok] if first else None, 1, len(PROMPT) + i, greedy=True)
         toks.append(tok)
     res["fail_s"] = time.time() - t0
     res["tokens"] = np.array(toks, np.int32)

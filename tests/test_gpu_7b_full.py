@@ -70,3 +70,41 @@ def test_7b_full_prompt512_vs_reference(model7b, ref):
     assert np.array_equal(bits(a[-1]), bits(b[-1])), "512-token prompt logits differ"
     m.close()
     rm.close()
+
+
+def _full_context(model, ref, last, check_chained=True):
+    """16-token prompt, then greedy decode at n_past 16..last on the GPU library and on the
+    reference build, both fed the reference's greedy token: the logits must be bit-identical
+    at every step (every n_kv the decode attention sees: its no-exchange path up to n_kv 128
+    and the score-exchange path beyond, ggml.c:1781-1815,7062-7130, llama.cpp:1010-1061), and
+    lvk_decode_greedy's chained token stream over the same positions must equal the
+    reference's."""
+    import lvk
+    from oracle_lib import prompt_tokens
+    m = lvk.Llama(model, n_ctx=512)
+    rm = ref.model(model, 512)
+    toks = prompt_tokens(16)
+    m.eval(toks, 0)
+    b = rm.eval(toks, 0, n_threads=_threads())
+    tok0 = tok = int(np.argmax(b[-1]))
+    stream, bad = [], []
+    for n_past in range(16, last + 1):
+        a = m.eval([tok], n_past)
+        b = rm.eval([tok], n_past, n_threads=_threads())
+        if not np.array_equal(bits(a[-1]), bits(b[-1])):
+            bad.append(n_past)
+        tok = int(np.argmax(b[-1]))
+        stream.append(tok)
+    assert not bad, "decode logits differ at n_past %s" % bad[:20]
+    if check_chained:
+        m.eval(toks, 0)
+        got = [int(t) for t in m.decode_greedy(tok0, 16, last + 1 - 16)]
+        assert got == stream, "chained greedy tokens differ from the reference from step %d" % next(
+            i for i, (x, y) in enumerate(zip(got, stream)) if x != y)
+    m.close()
+    rm.close()
+
+
+def test_7b_full_context_decode_to_511_vs_reference(model7b, ref):
+    """BASELINE configs[1] over the whole n_ctx 512 window: 496 decode steps (n_past 16..511)"""
+    _full_context(model7b, ref, 511)

@@ -34,3 +34,35 @@ def test_graph_compute_matches_reference_ggml(gpu_available, wtype, kv, tmp_path
     bad = np.flatnonzero(a.view(np.uint32) != b.view(np.uint32))
     assert bad.size == 0, "logits differ at %d places, first %s: %r vs %r" % (bad.size, bad[:5], a[bad[:5]], b[bad[:5]])
     assert np.array_equal(dumps[0], dumps[1]), "KV caches differ"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wtype", [0, 1])
+def test_graph_compute_uploads_weights_once(gpu_available, wtype, tmp_path):
+    """ggml_graph_compute keeps its device state across calls: the weights (a read-only
+    buffer of the caller, like llama.cpp's PROT_READ model mapping) go host -> device and
+    are repacked in the first call only; each later decode step uploads just what the host
+    may have changed (its token ids, the KV positions it reads -- well under the weight
+    bytes) and copies back just the bytes its nodes wrote.  The logits of the compared
+    steps stay those of the plain run (test above)."""
+    _build()
+    env = dict(os.environ, GRAPH_TEST_REPEAT="6")
+    r = subprocess.run([LVK_BIN, str(tmp_path / "x.bin"), str(wtype), "1"], capture_output=True, text=True,
+                       env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    calls = []
+    for ln in r.stderr.splitlines():
+        if ln.startswith("compute "):
+            f = ln.split()
+            calls.append({f[i]: float(f[i + 1]) for i in range(2, len(f) - 1, 2)})
+    assert len(calls) == 10, r.stderr[-2000:]
+    E, F, V, L = 256, 768, 512, 2
+    blk = 20 if wtype == 0 else 24
+    wbytes = (L * (4 * E * E + 3 * E * F) + 2 * E * V) // 32 * blk
+    assert calls[0]["h2d"] >= wbytes and calls[0]["repack"] >= wbytes - E * V // 32 * blk
+    for c in calls[4:]:
+        assert c["repack"] == 0, calls
+        assert c["h2d"] < wbytes / 4, calls
+        assert c["d2h"] < wbytes / 4, calls
+        assert c["mode"] in (1, 2), calls
+    print("per-call ms:", [round(c["ms"], 3) for c in calls], "h2d:", [int(c["h2d"]) for c in calls])

@@ -93,3 +93,18 @@ def test_stage_bad_token_fails_every_stage(tiny_models, gpu_available, tmp_path)
     for r in res:
         assert int(r["failed_at"]) == 3, [int(x["failed_at"]) for x in res]
         assert float(r["fail_s"]) < 30.0
+
+
+@pytest.mark.gpu
+def test_stage_link_reconnects_after_abort(tiny_models, gpu_available, tmp_path):
+    """after the aborted step 3 every stage reconnects under the SAME shm name (stage 0 makes
+    a fresh ring: no stale abort word, join count or messages) and redoes the step: the
+    greedy stream equals the unsplit context's"""
+    import lvk
+    path = tiny_models["tiny_q4_0"]
+    _, want_toks = _reference(lvk, path)
+    res = _run_stages(path, 3, "reconnect", tmp_path)
+    for r in res:
+        assert int(r["failed_at"]) == 3
+    assert list(res[0]["tokens"]) == want_toks
+    assert list(res[-1]["tokens"]) == want_toks

@@ -10,12 +10,21 @@
  * usage: graph_test <out.bin> <wtype 0=Q4_0 1=Q4_1> <kv type 1=F16 0=F32>
  * Steps: a 7-token prompt at n_past 0, a 33-token batch at n_past 7 (n_kv 40 crosses the
  * 32-element f16-dot tail), two single-token decode steps.
+ *
+ * The weights live in a buffer the caller maps itself and makes read-only once filled (as a
+ * PROT_READ model-file mapping is), the KV cache in a second, writable context.  With
+ * GRAPH_TEST_REPEAT=n, n more decode steps follow the dump, each timed, and -- when the
+ * library exports lvk_ggml_stats (llama.vk_amd; a weak reference, so the same source links
+ * against the reference ggml.c) -- the bytes each call moved are printed to stderr.
  */
+#define _GNU_SOURCE   /* mmap MAP_ANONYMOUS, clock_gettime under -std=c11 */
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <time.h>
 
 #include "ggml.h"
 
@@ -51,6 +60,8 @@ static void fill_f32(struct ggml_tensor * t, float lo, float hi) {
     for (int64_t i = 0; i < ggml_nelements(t); ++i) p[i] = next_f(lo, hi);
 }
 
+extern int lvk_ggml_stats(uint64_t * out, int n) __attribute__((weak));
+
 struct layer {
     struct ggml_tensor *an, *fn, *wq, *wk, *wv, *wo, *w1, *w2, *w3;
 };
@@ -65,7 +76,10 @@ int main(int argc, char ** argv) {
     const int build_only = getenv("GRAPH_TEST_BUILD_ONLY") != NULL;
     ggml_time_init();
 
-    struct ggml_init_params wp = {64u << 20, NULL, false};
+    const size_t wbytes = 64u << 20;
+    void * wbuf = mmap(NULL, wbytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (wbuf == MAP_FAILED) return 1;
+    struct ggml_init_params wp = {wbytes, wbuf, false};
     struct ggml_context * wctx = ggml_init(wp);
     struct ggml_tensor * tok = ggml_new_tensor_2d(wctx, wt, E, V);
     struct ggml_tensor * norm = ggml_new_tensor_1d(wctx, GGML_TYPE_F32, E);
@@ -95,17 +109,30 @@ int main(int argc, char ** argv) {
         fill_q(ly[l].w2, 0.5f / (sqrtf((float) F) * 4.6f), 1.5f / (sqrtf((float) F) * 4.6f));
         fill_q(ly[l].w3, 0.5f * ws, 1.5f * ws);
     }
-    struct ggml_tensor * kv_k = ggml_new_tensor_1d(wctx, kt, (int64_t) L * C * E);
-    struct ggml_tensor * kv_v = ggml_new_tensor_1d(wctx, kt, (int64_t) L * C * E);
+    /* every weight written: the buffer becomes read-only (ggml_init wrote its object list
+     * into it; no tensor is created in wctx after this) */
+    if (mprotect(wbuf, wbytes, PROT_READ) != 0) return 1;
+    struct ggml_init_params kp = {16u << 20, NULL, false};
+    struct ggml_context * kctx = ggml_init(kp);
+    struct ggml_tensor * kv_k = ggml_new_tensor_1d(kctx, kt, (int64_t) L * C * E);
+    struct ggml_tensor * kv_v = ggml_new_tensor_1d(kctx, kt, (int64_t) L * C * E);
     memset(kv_k->data, 0, ggml_nbytes(kv_k));
     memset(kv_v->data, 0, ggml_nbytes(kv_v));
 
     FILE * fo = fopen(argv[1], "wb");
     if (!fo) return 1;
     const int steps[4][2] = {{7, 0}, {33, 7}, {1, 40}, {1, 41}};
+    const int repeat = getenv("GRAPH_TEST_REPEAT") ? atoi(getenv("GRAPH_TEST_REPEAT")) : 0;
     int last = 1;
-    for (int st = 0; st < 4; ++st) {
-        const int N = steps[st][0], n_past = steps[st][1];
+    for (int st = 0; st < 4 + (repeat < C - 42 ? repeat : C - 42); ++st) {
+        const int N = st < 4 ? steps[st][0] : 1, n_past = st < 4 ? steps[st][1] : 42 + (st - 4);
+        if (st == 4) {
+            /* the dump covers the four compared steps only */
+            fwrite(kv_k->data, 1, ggml_nbytes(kv_k), fo);
+            fwrite(kv_v->data, 1, ggml_nbytes(kv_v), fo);
+            fclose(fo);
+            fo = NULL;
+        }
         struct ggml_init_params cp = {256u << 20, NULL, false};
         struct ggml_context * ctx0 = ggml_init(cp);
         struct ggml_cgraph gf;
@@ -166,9 +193,18 @@ int main(int argc, char ** argv) {
             fprintf(stderr, "topology %d: %016llx\n", st, (unsigned long long) h);
             memset(logits->data, 0, sizeof(float) * (size_t) V * N);
         } else {
+            struct timespec t0, t1;
+            clock_gettime(CLOCK_MONOTONIC, &t0);
             ggml_graph_compute(ctx0, &gf);
+            clock_gettime(CLOCK_MONOTONIC, &t1);
+            uint64_t sv[6] = {0};
+            if (lvk_ggml_stats) lvk_ggml_stats(sv, 6);
+            fprintf(stderr, "compute %d: ms %.3f h2d %llu d2h %llu repack %llu mirrored %llu mode %llu\n", st,
+                    (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6, (unsigned long long) sv[0],
+                    (unsigned long long) sv[1], (unsigned long long) sv[2], (unsigned long long) sv[3],
+                    (unsigned long long) sv[4]);
         }
-        fwrite(logits->data, sizeof(float), (size_t) V * N, fo);
+        if (fo) fwrite(logits->data, sizeof(float), (size_t) V * N, fo);
         /* next tokens: argmax of the last row */
         const float * lr = (const float *) logits->data + (size_t) V * (N - 1);
         int best = 0;
@@ -179,9 +215,13 @@ int main(int argc, char ** argv) {
                 gf.n_leafs, ggml_used_mem(ctx0), best);
         ggml_free(ctx0);
     }
-    fwrite(kv_k->data, 1, ggml_nbytes(kv_k), fo);
-    fwrite(kv_v->data, 1, ggml_nbytes(kv_v), fo);
-    fclose(fo);
+    if (fo) {
+        fwrite(kv_k->data, 1, ggml_nbytes(kv_k), fo);
+        fwrite(kv_v->data, 1, ggml_nbytes(kv_v), fo);
+        fclose(fo);
+    }
+    ggml_free(kctx);
     ggml_free(wctx);
+    munmap(wbuf, wbytes);
     return 0;
 }
