@@ -508,7 +508,7 @@ float * llama_get_logits(struct llama_context * ctx) { return ctx->c.logits.data
 float * llama_get_embeddings(struct llama_context * ctx) { return ctx->c.embedding.data(); }
 
 const char * llama_token_to_str(struct llama_context * ctx, llama_token token) {
-    if (token >= llama_n_vocab(ctx)) return nullptr;
+    if (token < 0 || token >= llama_n_vocab(ctx)) return nullptr;   // llama.cpp:1761-1766 checks the upper bound only
     return ctx->c.model.vocab.id_to_token[token].text.c_str();
 }
 

@@ -133,9 +133,12 @@ void read_tensor_index(Reader & rd, FileVer ver, size_t file_idx, std::map<std::
         if (ver >= V_GGJT) rd.off += (32 - (rd.off & 31)) & 31;     // llama.cpp:397-400
         sh.file = file_idx;
         sh.off = rd.off;
-        size_t rows = sh.ne.size() > 1 ? sh.ne[1] : 1;
-        sh.size = type_row_bytes(sh.type, sh.ne[0]) * rows;
-        if (rd.off + sh.size > rd.n) throw Error("tensor '" + name + "' data is not within the file bounds");
+        const size_t rows = sh.ne.size() > 1 ? sh.ne[1] : 1;
+        // in 128 bits: a corrupt shape must fail the bounds check, not wrap around it
+        const unsigned __int128 bytes = (unsigned __int128) type_row_bytes(sh.type, sh.ne[0]) * rows;
+        if (rd.off > rd.n || bytes > (unsigned __int128) (rd.n - rd.off))
+            throw Error("tensor '" + name + "' data is not within the file bounds");
+        sh.size = (size_t) bytes;
         rd.off += sh.size;
         if (order) order->push_back({name, sh.type, sh.ne, sh.off, sh.size});
         idx[name].push_back(sh);
@@ -178,6 +181,8 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
     // multi-part: n_parts = n_embd / tok_embeddings.ne[0] (llama.cpp:533-540)
     auto te = idx.find("tok_embeddings.weight");
     if (te == idx.end()) throw Error("missing tok_embeddings.weight");
+    if (te->second.at(0).ne.at(0) == 0 || m.hp.n_embd == 0 || m.hp.n_head == 0 || m.hp.n_layer == 0 || m.hp.n_mult == 0)
+        throw Error("invalid hyperparameters or tok_embeddings.weight shape");
     const uint32_t n_parts = m.hp.n_embd / te->second.at(0).ne.at(0);
     for (uint32_t i = 1; i < n_parts; ++i) {
         const std::string fname = path + "." + std::to_string(i);

@@ -31,6 +31,13 @@ struct In {
         off += 4;
         return v;
     }
+    // n bytes at the cursor, bounds-checked, then skipped
+    const uint8_t * take(size_t n) {
+        if (off > b.size() || n > b.size() - off) throw std::string("unexpected end of file");
+        const uint8_t * p = b.data() + off;
+        off += n;
+        return p;
+    }
 };
 
 void put(std::vector<uint8_t> & o, const void * p, size_t n) {
@@ -143,10 +150,9 @@ void quantize_file(const char * fin, const char * fout, int itype) {
     for (uint32_t i = 0; i < hp[0]; ++i) {
         const uint32_t len = in.u32();
         put_u32(out, len);
-        put(out, &in.b[in.off], len);
-        in.off += len;
+        put(out, in.take(len), len);
         float score = 0.0f;
-        if (has_scores) { std::memcpy(&score, &in.b[in.off], 4); in.off += 4; }
+        if (has_scores) std::memcpy(&score, in.take(4), 4);
         put(out, &score, 4);
     }
     std::vector<float> f32;
@@ -156,12 +162,12 @@ void quantize_file(const char * fin, const char * fout, int itype) {
         if (nd < 1 || nd > 2) throw std::string("bad tensor dims");
         uint32_t ne[2] = {1, 1};
         for (uint32_t i = 0; i < nd; ++i) ne[i] = in.u32();
-        const std::string name((const char *) &in.b[in.off], nl);
-        in.off += nl;
-        if (aligned) in.off += (32 - (in.off & 31)) & 31;
-        const size_t sz = row_bytes(ft, ne[0]) * ne[1];
-        const uint8_t * data = &in.b[in.off];
-        in.off += sz;
+        const std::string name((const char *) in.take(nl), nl);
+        if (aligned) in.take((32 - (in.off & 31)) & 31);
+        const unsigned __int128 sz128 = (unsigned __int128) row_bytes(ft, ne[0]) * ne[1];
+        if (sz128 > (unsigned __int128) in.b.size()) throw std::string("tensor '" + name + "' data is not within the file");
+        const size_t sz = (size_t) sz128;
+        const uint8_t * data = in.take(sz);
         const bool quant = name.size() >= 6 && name.compare(name.size() - 6, 6, "weight") == 0 && nd == 2;
         uint32_t new_t = ft;
         const uint8_t * nd_ptr = data;
