@@ -28,6 +28,8 @@ def test_graph_topology_and_pool_match_reference(wtype, kv, tmp_path):
     if not os.path.exists(REF_BIN):
         pytest.skip("reference build oracle/_ref/graph_test_ref not present")
     env = dict(os.environ, GRAPH_TEST_BUILD_ONLY="1")
+    if os.environ.get("LVK_LIB"):       # another build of the library (the sanitizer run)
+        env["LD_LIBRARY_PATH"] = os.path.dirname(os.environ["LVK_LIB"])
     outs = []
     for b in (REF_BIN, LVK_BIN):
         r = subprocess.run([b, str(tmp_path / "x.bin"), str(wtype), str(kv)], capture_output=True, text=True,

@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "llama.vk_amd", "lib", "libllama_vk_amd.so")
+LIB = os.environ.get("LVK_LIB") or os.path.join(ROOT, "llama.vk_amd", "lib", "libllama_vk_amd.so")
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref.so")
 TEST_QUANTIZE = os.path.join(ROOT, "tools", "dropin", "bin", "test-quantize")
 HAS = ["avx", "avx2", "avx512", "fma", "neon", "arm_fma", "f16c", "fp16_va", "wasm_simd", "blas", "sse3", "vsx"]
