@@ -72,6 +72,9 @@ class LocalCoord:
     def bcast(self, obj):
         return obj
 
+    def gather(self, obj):
+        return [obj]
+
 
 class PipeCoord:
     """N > 1, in the worker process: the barrier, max over ranks and broadcast from rank 0 are
@@ -102,6 +105,10 @@ class PipeCoord:
 
     def bcast(self, obj):
         return self._ask("bcast", obj)
+
+    def gather(self, obj):
+        """every rank's obj, in rank order, on every rank"""
+        return self._ask("gather", obj)
 
     def result(self, obj):
         self._ask("result", obj)
@@ -143,6 +150,10 @@ def serve_worker(argv):
             box = [v]
             dist.broadcast_object_list(box, src=0)
             v = box[0]
+        elif op == "gather":
+            out = [None] * ws
+            dist.all_gather_object(out, v)
+            v = out
         elif op == "result":
             result = v
         wr.write(json.dumps({"v": v}) + "\n")
@@ -334,6 +345,8 @@ def split_child(args):
     ptoks = np.array(prompt_tokens(16), np.int32)
     first = s == 0
     st.stage_step(ptoks if first else None, 16, 0, micro=args.split_micro)
+    # the last stage's prompt logits, as the bit pattern's digest (compared with one unsplit context)
+    lhash = logits_digest(st.logits()[-1]) if s == S - 1 else None
     tok, n_past = SPLIT_FIRST_TOKEN, 16
     toks = []
     for _ in range(args.warmup):
@@ -361,22 +374,29 @@ def split_child(args):
     st.close()
     print(json.dumps({"stage": s, "layers": list(lr), "load_s": load_s, "decode_s": dec,
                       "prefill_s": pre[args.split_micro], "prefill_nomicro_s": pre[0],
-                      "tokens": toks if first else None}), flush=True)
+                      "tokens": toks if first else None, "prompt_logits_digest": lhash}), flush=True)
+
+
+def logits_digest(row):
+    import hashlib
+    import numpy as np
+    return hashlib.sha256(np.ascontiguousarray(row, np.float32).view(np.uint32).tobytes()).hexdigest()[:32]
 
 
 def greedy_tokens_1gpu(path, n):
     """the same greedy steps as a split's stages (16-token prompt, then SPLIT_FIRST_TOKEN at
-    n_past 16, ...) on one unsplit context: what the split's token stream must equal"""
+    n_past 16, ...) on one unsplit context: what the split's token stream must equal; also
+    the digest of the prompt's last logits row"""
     import numpy as np
     import lvk
     m = lvk.Llama(path, n_ctx=512)
-    m.eval(np.array(prompt_tokens(16), np.int32), 0)
+    digest = logits_digest(m.eval(np.array(prompt_tokens(16), np.int32), 0)[-1])
     tok, out = SPLIT_FIRST_TOKEN, []
     for i in range(n):
         tok = m.eval_greedy(tok, 16 + i)
         out.append(tok)
     m.close()
-    return out
+    return out, digest
 
 
 def layer_split(args, coord):
@@ -419,14 +439,17 @@ def layer_split(args, coord):
     dec = coord.max(res["decode_s"])
     pre = coord.max(res["prefill_s"])
     pre0 = coord.max(res["prefill_nomicro_s"])
+    digest_split = coord.gather(res.get("prompt_logits_digest"))[-1]     # the last stage's
     check = None
     if rank == 0 and args.split_check > 0:
         n = min(args.split_check, len(res["tokens"]))
         t0 = time.time()
-        want = greedy_tokens_1gpu(path, n)
+        want, digest = greedy_tokens_1gpu(path, n)
         check = {"n_tokens": n, "tokens_split": res["tokens"][:n], "tokens_1gpu": want,
                  "match": res["tokens"][:n] == want, "check_s": time.time() - t0,
-                 "positions": "16..%d" % (16 + n - 1), "first_token": SPLIT_FIRST_TOKEN}
+                 "positions": "16..%d" % (16 + n - 1), "first_token": SPLIT_FIRST_TOKEN,
+                 "prompt_logits_digest_split": digest_split, "prompt_logits_digest_1gpu": digest,
+                 "prompt_logits_bit_identical": digest_split == digest}
     coord.barrier()
     L = CFG_65B["n_layer"]
     r = args.steps_split / dec
@@ -547,7 +570,7 @@ def main():
     ap.add_argument("--split-device", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--split-uid", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04_traffic.json"))
     args = ap.parse_args()
     if args.split_child:
         split_child(args)
@@ -571,8 +594,9 @@ def run(args, coord):
         coord.barrier()
         mx = coord.max(float(rank + 1))
         b = coord.bcast({"uid": "ab" * 64} if rank == 0 else None)
+        g = coord.gather({"r": rank})
         coord.barrier()
-        return {"ws": ws, "rank": rank, "max": mx, "bcast": b, "torch_in_worker": "torch" in sys.modules} \
+        return {"ws": ws, "rank": rank, "max": mx, "bcast": b, "gather": g, "torch_in_worker": "torch" in sys.modules} \
             if rank == 0 else None
     n_gpus = args.gpus if args.gpus else ws
     import numpy as np

@@ -130,6 +130,10 @@ hipError_t launch_matvec_q41(const MvLaunch & L, int pro, int epi, hipStream_t s
 bool matvec_cu_supported(int K, int qtype = Q4_0);
 hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s);
 bool matvec_cu41_supported(int K);
+// the Q4_0 decode matvec with its weights streamed into LDS by LDS-DMA (matvec_dma.hip):
+// Wo / W2 shapes with at most two row groups per CU; hipErrorNotSupported otherwise
+bool matvec_dma_enabled();
+hipError_t launch_matvec_dma(const MvLaunch & L, int pro, int epi, hipStream_t s);
 hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t s);
 // compute units of the current device (one decode workgroup per CU)
 int cu_count();

@@ -1,0 +1,290 @@
+// matvec_dma.hip -- single-token Q4_0 matvec whose weight stream lands in LDS by LDS-DMA,
+// for the decode shapes with few row groups per CU (Wo, W2: 2 per CU on the 7B shapes).
+//
+// Same arithmetic as matvec_cu.hip (ggml_vec_dot_q4_0 AVX2 chains, ggml.c:1950-2026, on an
+// activation quantized by quantize_row_q4_0, ggml.c:621-685; lane 8r+j = chain j of row r)
+// and the same octet image, row-group split (one workgroup per CU, contiguous row groups)
+// and epilogues.  What differs is where a wave's weights wait for their chain:
+//
+//   * matvec_cu keeps D chunks (5 KiB each) per wave in VGPRs.  With two compute waves per
+//     CU that is 20-40 KiB in flight per CU, and at the loaded HBM latency a CU then pulls
+//     10-20 GB/s: Wo (41 KiB per CU) and W2 (110 KiB per CU) are bound by the bytes a CU
+//     keeps in flight (Little's law), not by HBM.
+//   * here each compute wave DMAs its chunks (global_load_lds_dwordx4, 1 KiB per wave
+//     instruction, no VGPRs) into a ring of R slots of its own in LDS: R = 4 (Wo) or 11 (W2)
+//     is the whole row group, i.e. every weight byte of the launch is requested in the
+//     first microsecond while prologue waves load the input and build the activation
+//     table.  The chains then read their operands with ds_read_b128.
+//
+// The DMAs are inline asm, invisible to hipcc's wait-count pass: the wave waits for its own
+// chunk i with s_waitcnt vmcnt(5 (R - 1)) (every chunk is exactly 5 DMAs -- a row's partial
+// last chunk loads filler into its unused sub-chunk space -- and every refill is issued,
+// clamped to the wave's last chunk, so the count never varies), and the workgroup barrier
+// between the table and the chains is an LDS-only barrier (a __syncthreads would wait for
+// every DMA in flight).
+#include "lvk_device.h"
+#include "lvk_kernels.h"
+#include "matvec_common.h"
+
+#include <cstdlib>
+
+namespace lvk {
+
+namespace {
+using namespace mv;
+
+struct DmaParams {
+    const uint4 * nib;
+    const float4 * scl;
+    int G;                      // row groups (M / 8)
+    const float * x;            // PRO_ACTF: f32 input [K]
+    ActQ xq;                    // PRO_ACTQ: quantized input
+    float * y;                  // EPI_RESID / EPI_STORE
+};
+
+constexpr int SRS = 40, SPL = 8 * SRS;      // per-wave scale table (matvec_cu.hip)
+constexpr int SLOT = 5 * 1024;              // one chunk: 4 x 1 KiB nibbles + 1 KiB scales
+
+__device__ __forceinline__ unsigned lds_u32(const void * p) {
+    return (unsigned) (uintptr_t) (const __attribute__((address_space(3))) uint8_t *) p;
+}
+// one 1 KiB LDS-DMA: lane l's 16 bytes at gsrc land at LDS byte lds_dst + 16 l
+__device__ __forceinline__ void dma1k(const void * gsrc, unsigned lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int NW, int NP, int R, int PRO, int EPI, int KT>
+__global__ __launch_bounds__((NW + NP) * 64) void k_mv_dma(DmaParams P) {
+    constexpr int nb = KT / 32;                 // blocks per row
+    constexpr int nsub = nb / 8;                // 8-block sub-chunks
+    constexpr int NC = (nb + 31) / 32;          // chunks of 32 blocks
+    constexpr int PT = NP * 64;                 // prologue threads
+    static_assert(nb % 8 == 0, "K must be a multiple of 256");
+    static_assert(NP > 0, "prologue waves build the table");
+
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t * act = (uint32_t *) smem;                                 // nb * 32 B
+    float * dxp = (float *) (smem + nb * 32);                           // NC * 128 B
+    float * sbuf = dxp + NC * 32;                                       // NW * 2 * SPL floats
+    uint8_t * ring0 = (uint8_t *) (sbuf + NW * 2 * SPL);                // NW * R * SLOT
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    if (wave >= NW) {
+        // ---- prologue waves: the activation table (the compute waves' DMAs are in flight)
+        const int pt = tid - NW * 64;
+        if constexpr (PRO == PRO_ACTF) {
+            constexpr int nunits = KT / 8;
+            constexpr int UMP = (nunits + PT - 1) / PT;
+            float4 xv[UMP][2];
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                const int un = min(k * PT + pt, nunits - 1);
+                const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
+                xv[k][0] = xp[0]; xv[k][1] = xp[1];
+            }
+            // barrier A: the inputs enter the CU's texture queue ahead of the DMA burst
+            __builtin_amdgcn_s_barrier();
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                if (k * PT >= nunits) break;
+                const int un = k * PT + pt;
+                float v[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
+                              xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
+                float amax = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) { const float a = fabsf(v[e]); amax = a > amax ? a : amax; }
+                // the 4 units of a block are a lane quad: block amax (ggml.c:636-649)
+                const float o0 = quad_bcast<0>(amax), o1 = quad_bcast<1>(amax);
+                const float o2 = quad_bcast<2>(amax), o3 = quad_bcast<3>(amax);
+                const float m01 = o1 > o0 ? o1 : o0, m23 = o3 > o2 ? o3 : o2;
+                amax = m23 > m01 ? m23 : m01;
+                const float d = amax / 7.0f;                              // ggml.c:651
+                const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;     // ggml.c:653
+                const uint32_t w = q40_pack8(v, id);
+                if (un < nunits) act_store(act, dxp, un >> 2, un & 3, w, d, (un & 3) == 0);
+            }
+        } else {
+            constexpr int UMP = (nb + PT - 1) / PT;
+            uint4 qv[UMP];
+            float dv[UMP];
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                const int b = min(k * PT + pt, nb - 1);
+                qv[k] = P.xq.qs[b];
+                dv[k] = P.xq.d[b];
+            }
+            __builtin_amdgcn_s_barrier();       // barrier A (see above)
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                const int b = k * PT + pt;
+                if (b < nb) {
+                    const uint4 qs = qv[k];
+                    const float d = dv[k];
+                    act_store(act, dxp, b, 0, qs.x, d, true);
+                    act_store(act, dxp, b, 1, qs.y, 0.0f, false);
+                    act_store(act, dxp, b, 2, qs.z, 0.0f, false);
+                    act_store(act, dxp, b, 3, qs.w, 0.0f, false);
+                }
+            }
+        }
+        lds_barrier();          // table ready (the compute waves join this barrier)
+        return;
+    }
+
+    // ---- compute waves: row groups g0 + wave, g0 + wave + NW, ... of this workgroup
+    const int j = lane & 7;
+    const int r = lane >> 3;
+    const int nwg = gridDim.x;
+    const int g0 = (int) (blockIdx.x * (unsigned) P.G / (unsigned) nwg);     // G * n_cu < 2^32
+    const int g1 = (int) ((blockIdx.x + 1) * (unsigned) P.G / (unsigned) nwg);
+    const int ng = max(0, (g1 - g0 - wave + NW - 1) / NW);
+    __builtin_amdgcn_s_barrier();               // barrier A: the prologue's input loads went out first
+    if (ng == 0) { lds_barrier(); return; }
+    const int T = ng * NC;                       // chunks of this wave's stream
+    uint8_t * ring = ring0 + (size_t) wave * R * SLOT;
+    const unsigned ring_l = __builtin_amdgcn_readfirstlane(lds_u32(ring));
+    // chunk i (clamped to the last) into ring slot s: 4 nibble sub-chunks + the scales; a
+    // partial last chunk of a row loads its scales again into the unused sub-chunk space,
+    // so every chunk is 5 DMAs
+    auto issue = [&](int i, int s) __attribute__((always_inline)) {
+        i = min(i, T - 1);
+        const int grp = g0 + wave + (i / NC) * NW, cc = i % NC;
+        const uint4 * src = P.nib + ((size_t) grp * NC * 4 + cc * 4) * 64 + lane;
+        const float4 * ssrc = P.scl + ((size_t) grp * NC + cc) * 64 + lane;
+        const unsigned d = ring_l + (unsigned) s * SLOT;
+#pragma unroll
+        for (int sb = 0; sb < 4; ++sb) {
+            if (nsub % 4 == 0 || cc * 4 + sb < nsub) dma1k(src + sb * 64, d + sb * 1024);
+            else dma1k(ssrc, d + sb * 1024);
+        }
+        dma1k(ssrc, d + 4096);
+    };
+#pragma unroll
+    for (int s = 0; s < R; ++s) issue(s, s);
+
+    float * sw = sbuf + wave * 2 * SPL;
+    auto make_table = [&](int buf, int slot, int cc) __attribute__((always_inline)) {
+        const float4 Sv = *((const float4 *) (ring + (size_t) slot * SLOT + 4096) + lane);
+        const float4 dx = *(const float4 *) (dxp + cc * 32 + j * 4);
+        float4 sv;
+        sv.x = Sv.x * dx.x; sv.y = Sv.y * dx.y; sv.z = Sv.z * dx.z; sv.w = Sv.w * dx.w;   // ggml.c:1968
+        *(float4 *) (sw + buf * SPL + r * SRS + j * 4) = sv;
+    };
+
+    lds_barrier();              // the activation table (dxp) is ready
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(5 * (R - 1)) : "memory");     // chunk 0 landed
+    make_table(0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+
+    int tb = 0, slot = 0, i = 0;
+    for (int k = 0; k < ng; ++k) {
+        const int grp = g0 + wave + k * NW;
+        float acc = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const uint4 * wl = (const uint4 *) (ring + (size_t) slot * SLOT) + lane;
+            uint4 W[4];
+#pragma unroll
+            for (int sb = 0; sb < 4; ++sb)
+                if (c * 4 + sb < nsub) W[sb] = wl[sb * 64];
+            uint4 A[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (c * 4 + q / 2 < nsub) A[q] = *(const uint4 *) (act + ((c * 8 + q) * 8 + j) * 4);
+            const float * sl = sw + tb * SPL;
+            float sa[8][4];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const float4 v = *(const float4 *) (sl + r * SRS + jj * 4);
+                sa[jj][0] = v.x; sa[jj][1] = v.y; sa[jj][2] = v.z; sa[jj][3] = v.w;
+            }
+            // the slot's reads returned: refill it R chunks ahead (clamped: the count of
+            // DMAs in flight stays 5 per chunk)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            issue(i + R, slot);
+#pragma unroll
+            for (int sb = 0; sb < 4; ++sb) {
+                if (c * 4 + sb < nsub) {
+                    const uint32_t wd[4] = {W[sb].x, W[sb].y, W[sb].z, W[sb].w};
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp) {
+                        const int bi = sb * 8 + pp * 4;
+                        const uint4 a = A[sb * 2 + pp];
+                        const int p0 = dot8(wd[2 * pp], a.x);
+                        const int p1 = dot8(wd[2 * pp], a.y);
+                        const int p2 = dot8(wd[2 * pp + 1], a.z);
+                        const int p3 = dot8(wd[2 * pp + 1], a.w);
+                        acc = __builtin_fmaf(sa[(bi + 0) & 7][(bi + 0) >> 3], (float) p0, acc);
+                        acc = __builtin_fmaf(sa[(bi + 1) & 7][(bi + 1) >> 3], (float) p1, acc);
+                        acc = __builtin_fmaf(sa[(bi + 2) & 7][(bi + 2) >> 3], (float) p2, acc);
+                        acc = __builtin_fmaf(sa[(bi + 3) & 7][(bi + 3) >> 3], (float) p3, acc);
+                    }
+                }
+            }
+            ++i;
+            slot = slot + 1 == R ? 0 : slot + 1;
+            // the next chunk's scale table (chunk c+1 of this row group or chunk 0 of the next);
+            // its DMAs have landed once at most the R - 1 chunks after it are in flight
+            if (i < T) {
+                asm volatile("s_waitcnt vmcnt(%0)" :: "n"(5 * (R - 1)) : "memory");
+                make_table(tb ^ 1, slot, c + 1 < NC ? c + 1 : 0);
+            }
+            __builtin_amdgcn_wave_barrier();
+            tb ^= 1;
+            asm volatile("" : "+v"(acc));     // chunks in program order (matvec_cu.hip rule 4)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const float res = octet_reduce(acc);
+        const int row = grp * 8 + r;
+        if constexpr (EPI == EPI_STORE) {
+            if (j == 0) P.y[row] = res;
+        } else {
+            if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+        }
+    }
+    // the clamped refills must land before the workgroup's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int NW, int NP, int R, int PRO, int EPI, int KT>
+hipError_t go(const DmaParams & P, hipStream_t s) {
+    constexpr int nb = KT / 32, NC = (nb + 31) / 32;
+    const int nwg = std::min(cu_count(), P.G);
+    const size_t lds = (size_t) nb * 32 + NC * 128 + (size_t) NW * 2 * SPL * 4 + (size_t) NW * R * SLOT;
+    if (lds > 160 * 1024) return hipErrorNotSupported;
+    LVK_LAUNCH((k_mv_dma<NW, NP, R, PRO, EPI, KT>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// LVK_MV_DMA=0 keeps Wo / W2 on matvec_cu.hip (A/B runs)
+bool matvec_dma_enabled() {
+    static const bool on = [] { const char * e = getenv("LVK_MV_DMA"); return !e || atoi(e) != 0; }();
+    return on;
+}
+
+hipError_t launch_matvec_dma(const MvLaunch & L, int pro, int epi, hipStream_t s) {
+    if (L.w.qtype != Q4_0 || L.n_tokens != 1 || L.w.M % 8 || epi != EPI_RESID) return hipErrorNotSupported;
+    DmaParams P{};
+    P.nib = L.w.nib;
+    P.scl = (const float4 *) L.w.scl;
+    P.G = L.w.M / 8;
+    P.x = L.x ? L.x + (size_t) L.tok0 * L.w.K : nullptr;
+    P.xq = L.xq;
+    if (P.xq.qs) { P.xq.qs += (size_t) L.tok0 * L.xq.nb; P.xq.d += (size_t) L.tok0 * L.xq.nb; }
+    P.y = L.y ? L.y + (size_t) L.out_tok0 * L.w.M : nullptr;
+    const int per_cu = (P.G + std::min(cu_count(), P.G) - 1) / std::min(cu_count(), P.G);
+    // two compute waves (one row group each on the 7B shapes), the whole row group in flight
+    if (L.w.K == 4096 && pro == PRO_ACTQ && per_cu <= 2) return go<2, 2, 4, PRO_ACTQ, EPI_RESID, 4096>(P, s);
+    if (L.w.K == 11008 && pro == PRO_ACTF && per_cu <= 2) return go<2, 6, 11, PRO_ACTF, EPI_RESID, 11008>(P, s);
+    return hipErrorNotSupported;
+}
+
+}  // namespace lvk

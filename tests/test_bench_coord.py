@@ -34,4 +34,5 @@ def test_bench_worker_coordination(ws):
     assert out["ws"] == ws and out["rank"] == 0
     assert out["max"] == float(ws)
     assert out["bcast"] == {"uid": "ab" * 64}
+    assert out["gather"] == [{"r": r} for r in range(ws)]
     assert out["torch_in_worker"] is False
