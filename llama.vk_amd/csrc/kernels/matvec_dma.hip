@@ -252,6 +252,236 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_dma(DmaParams P) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---- Q4_1 (13B): the k_mv_cu41 chains (ggml_vec_dot_q4_1 AVX2, ggml.c:2188-2258) with
+// the chunk's nibbles, d, m and even-chain weight sums (7 KiB, 7 DMAs) from the LDS ring
+constexpr int SWF41 = 4 * SPL;                 // per-wave product tables: s, dx*my, mx*dy, mx*my
+constexpr int SLOT41 = 7 * 1024;
+
+struct Dma41Params {
+    const uint4 * nib;
+    const float4 * scl;         // [G][NC][2][64]: d, then m
+    const uint4 * wsum;         // [G][NC][64]
+    int G;
+    const float * x;            // PRO_ACTF
+    ActQ xq;                    // PRO_ACTQ (d, m, qs)
+    float * y;
+};
+
+template <int NW, int NP, int R, int PRO, int EPI, int KT>
+__global__ __launch_bounds__((NW + NP) * 64) void k_mv_dma41(Dma41Params P) {
+    constexpr int nb = KT / 32;
+    constexpr int nsub = nb / 8;
+    constexpr int NC = (nb + 31) / 32;
+    constexpr int PT = NP * 64;
+    static_assert(nb % 8 == 0 && NP > 0, "shape");
+
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t * act = (uint32_t *) smem;                          // nb * 32 B
+    float * dyv = (float *) (smem + nb * 32);                    // NC * 32
+    float * myv = dyv + NC * 32;                                 // NC * 32
+    uint8_t * ys = (uint8_t *) (myv + NC * 32);                  // nb * 4 bytes (room: nb * 16)
+    float * sbuf = (float *) (ys + nb * 16);                     // NW * SWF41
+    uint8_t * ring0 = (uint8_t *) (sbuf + NW * SWF41);           // NW * R * SLOT41
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    if (wave >= NW) {
+        const int pt = tid - NW * 64;
+        if constexpr (PRO == PRO_ACTF) {
+            constexpr int nunits = KT / 8;
+            constexpr int UMP = (nunits + PT - 1) / PT;
+            float4 xv[UMP][2];
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                const int un = min(k * PT + pt, nunits - 1);
+                const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
+                xv[k][0] = xp[0]; xv[k][1] = xp[1];
+            }
+            __builtin_amdgcn_s_barrier();       // barrier A: inputs ahead of the DMA burst
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                if (k * PT >= nunits) break;
+                const int un = k * PT + pt;
+                float v[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
+                              xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
+                // quantize_row_q4_1 of the block held by this lane quad (ggml.c:847-920)
+                float d, m;
+                uint32_t qw;
+                q41_quad(v, d, m, qw);
+                uint32_t qs[4];
+                qs[0] = __builtin_bit_cast(uint32_t, quad_bcast<0>(__builtin_bit_cast(float, qw)));
+                qs[1] = __builtin_bit_cast(uint32_t, quad_bcast<1>(__builtin_bit_cast(float, qw)));
+                qs[2] = __builtin_bit_cast(uint32_t, quad_bcast<2>(__builtin_bit_cast(float, qw)));
+                qs[3] = __builtin_bit_cast(uint32_t, quad_bcast<3>(__builtin_bit_cast(float, qw)));
+                if (un < nunits && (un & 3) == 0) act41_store(act, dyv, myv, ys, un >> 2, qs, d, m);
+            }
+        } else {
+            constexpr int UMP = (nb + PT - 1) / PT;
+            uint4 qv[UMP];
+            float dv[UMP], mv_[UMP];
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                const int b = min(k * PT + pt, nb - 1);
+                qv[k] = P.xq.qs[b];
+                dv[k] = P.xq.d[b];
+                mv_[k] = P.xq.m[b];
+            }
+            __builtin_amdgcn_s_barrier();       // barrier A
+#pragma unroll
+            for (int k = 0; k < UMP; ++k) {
+                const int b = k * PT + pt;
+                if (b < nb) {
+                    const uint32_t qs[4] = {qv[k].x, qv[k].y, qv[k].z, qv[k].w};
+                    act41_store(act, dyv, myv, ys, b, qs, dv[k], mv_[k]);
+                }
+            }
+        }
+        lds_barrier();          // table ready
+        return;
+    }
+
+    const int j = lane & 7;
+    const int r = lane >> 3;
+    const int nwg = gridDim.x;
+    const int g0 = (int) (blockIdx.x * (unsigned) P.G / (unsigned) nwg);
+    const int g1 = (int) ((blockIdx.x + 1) * (unsigned) P.G / (unsigned) nwg);
+    const int ng = max(0, (g1 - g0 - wave + NW - 1) / NW);
+    __builtin_amdgcn_s_barrier();               // barrier A
+    if (ng == 0) { lds_barrier(); return; }
+    const int T = ng * NC;
+    uint8_t * ring = ring0 + (size_t) wave * R * SLOT41;
+    const unsigned ring_l = __builtin_amdgcn_readfirstlane(lds_u32(ring));
+    // chunk i (clamped) into slot s: 4 nibble sub-chunks (filler past a row's end), d, m, wsum
+    auto issue = [&](int i, int s) __attribute__((always_inline)) {
+        i = min(i, T - 1);
+        const int grp = g0 + wave + (i / NC) * NW, cc = i % NC;
+        const uint4 * src = P.nib + ((size_t) grp * NC * 4 + cc * 4) * 64 + lane;
+        const float4 * ssrc = P.scl + ((size_t) grp * NC + cc) * 128 + lane;
+        const uint4 * wsrc = P.wsum + ((size_t) grp * NC + cc) * 64 + lane;
+        const unsigned d = ring_l + (unsigned) s * SLOT41;
+#pragma unroll
+        for (int sb = 0; sb < 4; ++sb) {
+            if (nsub % 4 == 0 || cc * 4 + sb < nsub) dma1k(src + sb * 64, d + sb * 1024);
+            else dma1k(wsrc, d + sb * 1024);
+        }
+        dma1k(ssrc, d + 4096);
+        dma1k(ssrc + 64, d + 5120);
+        dma1k(wsrc, d + 6144);
+    };
+#pragma unroll
+    for (int s = 0; s < R; ++s) issue(s, s);
+
+    lds_barrier();              // the activation table is ready
+    const bool even = (j & 1) == 0;
+    const uint32_t * ys32 = (const uint32_t *) ys;
+    float * sw = sbuf + wave * SWF41;
+    int slot = 0, i = 0;
+    for (int k = 0; k < ng; ++k) {
+        const int grp = g0 + wave + k * NW;
+        float acc = 0.0f, off = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            // chunk i landed once at most the R - 1 chunks after it are in flight
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(7 * (R - 1)) : "memory");
+            const uint4 * wl = (const uint4 *) (ring + (size_t) slot * SLOT41) + lane;
+            uint4 W[4];
+#pragma unroll
+            for (int sb = 0; sb < 4; ++sb)
+                if (c * 4 + sb < nsub) W[sb] = wl[sb * 64];
+            const float4 SD = *(const float4 *) (wl + 256);
+            const float4 SM = *(const float4 *) (wl + 320);
+            const uint4 WS = wl[384];
+            // products of blocks 32c + 8m + j of this lane's row (ggml.c:2205-2212)
+            const float4 dy = *(const float4 *) (dyv + c * 32 + j * 4);
+            const float4 my = *(const float4 *) (myv + c * 32 + j * 4);
+            float * sl = sw + r * SRS + j;
+            const float dxa[4] = {SD.x, SD.y, SD.z, SD.w};
+            const float mxa[4] = {SM.x, SM.y, SM.z, SM.w};
+            const float dya[4] = {dy.x, dy.y, dy.z, dy.w};
+            const float mya[4] = {my.x, my.y, my.z, my.w};
+#pragma unroll
+            for (int mq = 0; mq < 4; ++mq) {
+                sl[mq * 8] = dxa[mq] * dya[mq];
+                sl[SPL + mq * 8] = dxa[mq] * mya[mq];
+                sl[2 * SPL + mq * 8] = mxa[mq] * dya[mq];
+                sl[3 * SPL + mq * 8] = mxa[mq] * mya[mq];
+            }
+            // the slot's operands are in registers: refill it R chunks ahead (clamped)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            issue(i + R, slot);
+            __builtin_amdgcn_wave_barrier();
+            const float * srow = sw + r * SRS;
+            const float * xrow = srow + (even ? SPL : 2 * SPL);
+            const float * mrow = srow + 3 * SPL;
+            // even chains: the precomputed weight sums (blocks 0-15 of the chunk in their own
+            // word, 16-31 in the odd neighbour's: DPP quad_perm [1,1,3,3]); odd chains: the
+            // activation sums from LDS (ggml.c:2236-2240), one byte per block
+            const uint32_t wown[4] = {WS.x, WS.y, WS.z, WS.w};
+            uint32_t wnb[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) wnb[q] = (uint32_t) __builtin_amdgcn_mov_dpp((int) wown[q], 0xF5, 0xF, 0xF, false);
+#pragma unroll
+            for (int sb = 0; sb < 4; ++sb) {
+                if (c * 4 + sb < nsub) {
+                    const uint32_t wd[4] = {W[sb].x, W[sb].y, W[sb].z, W[sb].w};
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp) {
+                        const int uu = c * 8 + sb * 2 + pp;
+                        const int bi = sb * 8 + pp * 4;
+                        const uint4 a = *(const uint4 *) (act + ((size_t) uu * 8 + j) * 4);
+                        const float4 s4 = *(const float4 *) (srow + bi);
+                        const float4 x4 = *(const float4 *) (xrow + bi);
+                        const float4 m4 = *(const float4 *) (mrow + bi);
+                        const uint32_t ydw = ys32[(size_t) uu * 4 + (j >> 1)];
+                        const uint32_t wdw = sb < 2 ? wown[(sb & 1) * 2 + pp] : wnb[(sb & 1) * 2 + pp];
+                        const uint32_t sdw = even ? wdw : ydw;
+                        const float S[4] = {(float) (sdw & 0xFFu), (float) ((sdw >> 8) & 0xFFu),
+                                            (float) ((sdw >> 16) & 0xFFu), (float) (sdw >> 24)};
+                        const int p[4] = {udot8(wd[2 * pp], a.x), udot8(wd[2 * pp], a.y),
+                                          udot8(wd[2 * pp + 1], a.z), udot8(wd[2 * pp + 1], a.w)};
+                        const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+                        const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+                        const float ms[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            acc = __builtin_fmaf(sv[q], (float) p[q], acc);    // ggml.c:2244
+                            acc = __builtin_fmaf(xs[q], S[q], acc);            // ggml.c:2247
+                            off = off + ms[q];                                 // ggml.c:2226
+                        }
+                    }
+                }
+            }
+            ++i;
+            slot = slot + 1 == R ? 0 : slot + 1;
+            // the product tables are rewritten by the next chunk
+            asm volatile("" : "+v"(acc), "+v"(off));
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const float res = octet_reduce(acc) + off * 32.0f;      // acc_offset * QK (ggml.c:2249)
+        const int row = grp * 8 + r;
+        if constexpr (EPI == EPI_STORE) {
+            if (j == 0) P.y[row] = res;
+        } else {
+            if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int NW, int NP, int R, int PRO, int EPI, int KT>
+hipError_t go41(const Dma41Params & P, hipStream_t s) {
+    constexpr int nb = KT / 32, NC = (nb + 31) / 32;
+    const int nwg = std::min(cu_count(), P.G);
+    const size_t lds = (size_t) nb * 32 + 2 * NC * 128 + (size_t) nb * 16 + (size_t) NW * SWF41 * 4 +
+                       (size_t) NW * R * SLOT41;
+    if (lds > 160 * 1024) return hipErrorNotSupported;
+    LVK_LAUNCH((k_mv_dma41<NW, NP, R, PRO, EPI, KT>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
+    return hipGetLastError();
+}
+
 template <int NW, int NP, int R, int PRO, int EPI, int KT>
 hipError_t go(const DmaParams & P, hipStream_t s) {
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
@@ -270,7 +500,31 @@ bool matvec_dma_enabled() {
     return on;
 }
 
+hipError_t launch_matvec_dma41(const MvLaunch & L, int pro, int epi, hipStream_t s) {
+    if (L.w.qtype != Q4_1 || L.n_tokens != 1 || L.w.M % 8 || epi != EPI_RESID) return hipErrorNotSupported;
+    Dma41Params P{};
+    P.nib = L.w.nib;
+    P.scl = (const float4 *) L.w.scl;
+    P.wsum = q41_wsum(L.w);
+    P.G = L.w.M / 8;
+    P.x = L.x ? L.x + (size_t) L.tok0 * L.w.K : nullptr;
+    P.xq = L.xq;
+    if (P.xq.qs) {
+        P.xq.qs += (size_t) L.tok0 * L.xq.nb;
+        P.xq.d += (size_t) L.tok0 * L.xq.nb;
+        P.xq.m += (size_t) L.tok0 * L.xq.nb;
+    }
+    P.y = L.y ? L.y + (size_t) L.out_tok0 * L.w.M : nullptr;
+    const int nwg = std::min(cu_count(), P.G);
+    const int per_cu = (P.G + nwg - 1) / nwg;
+    // 13B: 2-3 row groups per CU, one per compute wave
+    if (L.w.K == 5120 && pro == PRO_ACTQ && per_cu <= 3) return go41<3, 2, 5, PRO_ACTQ, EPI_RESID, 5120>(P, s);
+    if (L.w.K == 13824 && pro == PRO_ACTF && per_cu <= 3) return go41<3, 5, 4, PRO_ACTF, EPI_RESID, 13824>(P, s);
+    return hipErrorNotSupported;
+}
+
 hipError_t launch_matvec_dma(const MvLaunch & L, int pro, int epi, hipStream_t s) {
+    if (L.w.qtype == Q4_1) return launch_matvec_dma41(L, pro, epi, s);
     if (L.w.qtype != Q4_0 || L.n_tokens != 1 || L.w.M % 8 || epi != EPI_RESID) return hipErrorNotSupported;
     DmaParams P{};
     P.nib = L.w.nib;
