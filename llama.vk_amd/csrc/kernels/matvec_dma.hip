@@ -37,9 +37,18 @@ struct DmaParams {
     const uint4 * nib;
     const float4 * scl;
     int G;                      // row groups (M / 8)
-    const float * x;            // PRO_ACTF: f32 input [K]
+    const float * x;            // PRO_ACTF / PRO_NORM: f32 input [K]
+    const float * g;            // PRO_NORM: norm weight [K]
     ActQ xq;                    // PRO_ACTQ: quantized input
     float * y;                  // EPI_RESID / EPI_STORE
+    // EPI_QKV (matvec_cu.hip): RoPE + KV append of the stacked Wq|Wk|Wv rows
+    const StepParams * sp;
+    uint16_t * q16;
+    uint16_t * kc;
+    uint16_t * vc;
+    const float2 * rope;
+    int n_embd, head_dim, n_ctx;
+    int kv32;
 };
 
 constexpr int SRS = 40, SPL = 8 * SRS;      // per-wave scale table (matvec_cu.hip)
@@ -78,24 +87,60 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_dma(DmaParams P) {
     if (wave >= NW) {
         // ---- prologue waves: the activation table (the compute waves' DMAs are in flight)
         const int pt = tid - NW * 64;
-        if constexpr (PRO == PRO_ACTF) {
+        if constexpr (PRO == PRO_ACTF || PRO == PRO_NORM) {
             constexpr int nunits = KT / 8;
             constexpr int UMP = (nunits + PT - 1) / PT;
             float4 xv[UMP][2];
+            float4 gv[PRO == PRO_NORM ? UMP : 1][2];
 #pragma unroll
             for (int k = 0; k < UMP; ++k) {
                 const int un = min(k * PT + pt, nunits - 1);
                 const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
                 xv[k][0] = xp[0]; xv[k][1] = xp[1];
+                if constexpr (PRO == PRO_NORM) {
+                    const float4 * gp = (const float4 *) (P.g + (size_t) un * 8);
+                    gv[k][0] = gp[0]; gv[k][1] = gp[1];
+                }
+            }
+            constexpr int XPL = PRO == PRO_NORM ? KT / 4 / 64 : 1;
+            float4 xs[XPL];
+            if constexpr (PRO == PRO_NORM) {
+#pragma unroll
+                for (int q = 0; q < XPL; ++q) xs[q] = ((const float4 *) P.x)[q * 64 + lane];
             }
             // barrier A: the inputs enter the CU's texture queue ahead of the DMA burst
             __builtin_amdgcn_s_barrier();
+            float scale = 1.0f;
+            if constexpr (PRO == PRO_NORM) {
+                // ggml_compute_forward_rms_norm_f32 (ggml.c:6058-6076): every prologue wave
+                // sums all K squares itself (lane-strided, then a butterfly that leaves the
+                // same double in every lane); float squares carried in double
+                double acc = 0.0;
+#pragma unroll
+                for (int q = 0; q < XPL; ++q) {
+                    const float e[4] = {xs[q].x, xs[q].y, xs[q].z, xs[q].w};
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) { const float sq = e[t] * e[t]; acc += (double) sq; }
+                }
+                acc = warp_sum_d(acc);
+                const float mean = (float) (acc / (double) KT);
+                scale = 1.0f / sqrtf(mean + 1e-6f);
+            }
 #pragma unroll
             for (int k = 0; k < UMP; ++k) {
                 if (k * PT >= nunits) break;
                 const int un = k * PT + pt;
                 float v[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
                               xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
+                if constexpr (PRO == PRO_NORM) {
+                    const float gg[8] = {gv[k][0].x, gv[k][0].y, gv[k][0].z, gv[k][0].w,
+                                         gv[k][1].x, gv[k][1].y, gv[k][1].z, gv[k][1].w};
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float yn = v[e] * scale;      // ggml_vec_scale_f32 (ggml.c:6076)
+                        v[e] = gg[e] * yn;                  // ggml_mul(repeat(g), cur) (llama.cpp:984)
+                    }
+                }
                 float amax = 0.0f;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) { const float a = fabsf(v[e]); amax = a > amax ? a : amax; }
@@ -244,8 +289,28 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_dma(DmaParams P) {
         const int row = grp * 8 + r;
         if constexpr (EPI == EPI_STORE) {
             if (j == 0) P.y[row] = res;
-        } else {
+        } else if constexpr (EPI == EPI_RESID) {
             if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+        } else if constexpr (EPI == EPI_QKV) {
+            const int E = P.n_embd, hd = P.head_dim;
+            const int which = row / E;          // 0 q, 1 k, 2 v (uniform per wave: E % 8 == 0)
+            const int e = row - which * E;
+            const int pos = P.sp->n_past;
+            const float other = __shfl_xor(res, 8);   // row e^1 lives in lanes of row r^1
+            if (j == 0) {
+                if (which < 2) {
+                    // ggml_compute_forward_rope_f32 mode 0 (ggml.c:7209-7223)
+                    const int i0 = e % hd;
+                    const float2 cs = P.rope[(size_t) pos * (hd / 2) + (i0 >> 1)];
+                    float out;
+                    if ((i0 & 1) == 0) { const float a = res * cs.x, b = other * cs.y; out = a - b; }
+                    else               { const float a = other * cs.y, b = res * cs.x; out = a + b; }
+                    if (which == 0) kv_store(P.q16, e, out, P.kv32);
+                    else            kv_store(P.kc, (size_t) pos * E + e, out, P.kv32);
+                } else {
+                    kv_store(P.vc, (size_t) e * P.n_ctx + pos, res, P.kv32);     // llama.cpp:996-1008
+                }
+            }
         }
     }
     // the clamped refills must land before the workgroup's LDS is released
@@ -525,16 +590,27 @@ hipError_t launch_matvec_dma41(const MvLaunch & L, int pro, int epi, hipStream_t
 
 hipError_t launch_matvec_dma(const MvLaunch & L, int pro, int epi, hipStream_t s) {
     if (L.w.qtype == Q4_1) return launch_matvec_dma41(L, pro, epi, s);
-    if (L.w.qtype != Q4_0 || L.n_tokens != 1 || L.w.M % 8 || epi != EPI_RESID) return hipErrorNotSupported;
+    if (L.w.qtype != Q4_0 || L.n_tokens != 1 || L.w.M % 8 || (epi != EPI_RESID && epi != EPI_QKV))
+        return hipErrorNotSupported;
     DmaParams P{};
     P.nib = L.w.nib;
     P.scl = (const float4 *) L.w.scl;
     P.G = L.w.M / 8;
     P.x = L.x ? L.x + (size_t) L.tok0 * L.w.K : nullptr;
+    P.g = L.g;
     P.xq = L.xq;
     if (P.xq.qs) { P.xq.qs += (size_t) L.tok0 * L.xq.nb; P.xq.d += (size_t) L.tok0 * L.xq.nb; }
     P.y = L.y ? L.y + (size_t) L.out_tok0 * L.w.M : nullptr;
+    P.sp = L.sp;
+    P.q16 = L.q16; P.kc = L.kc; P.vc = L.vc; P.rope = L.rope.cs;
+    P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx; P.kv32 = L.kv32;
     const int per_cu = (P.G + std::min(cu_count(), P.G) - 1) / std::min(cu_count(), P.G);
+    // QKV (LVK_MV_DMA_QKV=1, A/B): six row groups per CU, one per compute wave, all in flight
+    if (epi == EPI_QKV) {
+        static const bool qkv = [] { const char * e = getenv("LVK_MV_DMA_QKV"); return e && atoi(e) != 0; }();
+        if (qkv && L.w.K == 4096 && pro == PRO_NORM && per_cu <= 6) return go<6, 2, 4, PRO_NORM, EPI_QKV, 4096>(P, s);
+        return hipErrorNotSupported;
+    }
     // two compute waves (one row group each on the 7B shapes), the whole row group in flight
     if (L.w.K == 4096 && pro == PRO_ACTQ && per_cu <= 2) return go<2, 2, 4, PRO_ACTQ, EPI_RESID, 4096>(P, s);
     if (L.w.K == 11008 && pro == PRO_ACTF && per_cu <= 2) return go<2, 6, 11, PRO_ACTF, EPI_RESID, 11008>(P, s);
