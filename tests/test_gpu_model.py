@@ -24,13 +24,16 @@ def lvk(gpu_available):
     return m
 
 
-@pytest.mark.parametrize("name,graph", [("tiny_q4_0", True), ("tiny_q4_0", False), ("tiny_q4_1", True),
-                                        ("tiny_l80_q4_0", True)])
-def test_tiny_matches_reference_golden(lvk, tiny_models, name, graph):
+# exact: the prompt chunks of >= 16 tokens on the VALU kernels (True) or on the shipped MFMA
+# kernels (False, the default); both are bit-identical to the reference
+@pytest.mark.parametrize("name,graph,exact", [("tiny_q4_0", True, True), ("tiny_q4_0", True, False),
+                                              ("tiny_q4_0", False, False), ("tiny_q4_1", True, True),
+                                              ("tiny_q4_1", True, False), ("tiny_l80_q4_0", True, False)])
+def test_tiny_matches_reference_golden(lvk, tiny_models, name, graph, exact):
     g = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
     m = lvk.Llama(tiny_models[name], n_ctx=512)
     m.set_graph(graph)
-    m.set_prompt_exact(True)     # bit-exact prompt chunks (the MFMA path: test_mfma_prompt_*)
+    m.set_prompt_exact(exact)
     n_past, off = 0, 0
     for step, n in enumerate(g["chunks"]):
         lg = m.eval(g["tokens"][off:off + n], n_past)
@@ -43,7 +46,6 @@ def test_tiny_matches_reference_golden(lvk, tiny_models, name, graph):
 def test_tiny_q4_0_long_decode_vs_oracle(lvk, oracle, tiny_models):
     path = tiny_models["tiny_q4_0"]
     m = lvk.Llama(path, n_ctx=256)
-    m.set_prompt_exact(True)
     om = oracle.model(path, 256)
     toks = np.array([1, 450, 4996, 17354, 1701, 29916], np.int32)
     a = m.eval(toks, 0)
@@ -62,10 +64,11 @@ def test_tiny_q4_0_long_decode_vs_oracle(lvk, oracle, tiny_models):
     om.close()
 
 
-def test_logits_all_and_embeddings(lvk, oracle, tiny_models):
+@pytest.mark.parametrize("exact", [True, False])
+def test_logits_all_and_embeddings(lvk, oracle, tiny_models, exact):
     path = tiny_models["tiny_q4_0"]
     m = lvk.Llama(path, n_ctx=128, logits_all=True, embedding=True)
-    m.set_prompt_exact(True)
+    m.set_prompt_exact(exact)
     om = oracle.model(path, 128)
     toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 40)], np.int32)
     a = m.eval(toks, 0)
@@ -81,13 +84,11 @@ def test_logits_all_and_embeddings(lvk, oracle, tiny_models):
 def test_kv_cache_roundtrip(lvk, tiny_models):
     path = tiny_models["tiny_q4_0"]
     m = lvk.Llama(path, n_ctx=128)
-    m.set_prompt_exact(True)
     toks = np.arange(1, 20, dtype=np.int32)
     m.eval(toks, 0)
     kv = m.kv_cache()
     a = m.eval([42], 19)
     m2 = lvk.Llama(path, n_ctx=128)
-    m2.set_prompt_exact(True)
     m2.set_kv_cache(kv, 19)
     b = m2.eval([42], 19)
     assert np.array_equal(bits(a), bits(b))
@@ -104,16 +105,18 @@ def test_eval_errors(lvk, tiny_models):
     m.close()
 
 
-def test_7b_shaped_decode_vs_oracle(lvk, oracle, model_dir):
+@pytest.mark.parametrize("n_prompt", [8, 24])
+def test_7b_shaped_decode_vs_oracle(lvk, oracle, model_dir, n_prompt):
     """LLaMA-7B layer shapes (n_embd 4096, n_ff 11008, 32 heads) with 2 layers:
     the decode path runs the CU-balanced kernels compiled for K = 4096 / 11008
-    (matvec_cu.hip); prompt chunks run the generic kernels.  Bit-exact vs oracle."""
-    from oracle_lib import gen_model
+    (matvec_cu.hip, matvec_dma.hip); the 8-token prompt runs the generic kernels, the
+    24-token one the MFMA matmuls.  Bit-exact vs oracle."""
+    from oracle_lib import gen_model, prompt_tokens
     path = gen_model(os.path.join(model_dir, "w4096_l2.bin"), n_embd=4096, n_head=32, n_layer=2, ftype=2, seed=7)
     m = lvk.Llama(path, n_ctx=512)
-    m.set_prompt_exact(True)
     om = oracle.model(path, 512)
-    toks = np.array([1, 450, 4996, 17354, 1701, 29916, 338, 263], np.int32)
+    toks = np.array([1, 450, 4996, 17354, 1701, 29916, 338, 263], np.int32) if n_prompt == 8 else \
+        np.array(prompt_tokens(n_prompt), np.int32)
     a = m.eval(toks, 0)
     b = om.eval(toks, 0)
     assert np.array_equal(bits(a), bits(b))
