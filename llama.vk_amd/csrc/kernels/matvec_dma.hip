@@ -17,16 +17,17 @@
 //     table.  The chains then read their operands with ds_read_b128.
 //
 // The DMAs are inline asm, invisible to hipcc's wait-count pass: the wave waits for its own
-// chunk i with s_waitcnt vmcnt(5 (R - 1)) (every chunk is exactly 5 DMAs -- a row's partial
-// last chunk loads filler into its unused sub-chunk space -- and every refill is issued,
-// clamped to the wave's last chunk, so the count never varies), and the workgroup barrier
-// between the table and the chains is an LDS-only barrier (a __syncthreads would wait for
-// every DMA in flight).
+// chunk i with s_waitcnt vmcnt(5 x the chunks issued after it) (every chunk is exactly 5
+// DMAs -- a row's partial last chunk loads filler into its unused sub-chunk space), and the
+// workgroup barrier between the table and the chains is an LDS-only barrier (a
+// __syncthreads would wait for every DMA in flight).
 #include "lvk_device.h"
 #include "lvk_kernels.h"
 #include "matvec_common.h"
 
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 
 namespace lvk {
 
@@ -64,6 +65,16 @@ __device__ __forceinline__ void dma1k(const void * gsrc, unsigned lds_dst) {
                  : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// s_waitcnt vmcnt(N): the DMAs are invisible to hipcc's wait-count pass
+template <int N> __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+// f(std::integral_constant<int, 0>), ..., f(std::integral_constant<int, N - 1>): a chunk loop
+// whose index is a constant expression (wait counts are instruction immediates)
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F && f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F && f) { static_for_impl(f, std::make_integer_sequence<int, N>{}); }
 
 template <int NW, int NP, int R, int PRO, int EPI, int KT>
 __global__ __launch_bounds__((NW + NP) * 64) void k_mv_dma(DmaParams P) {
@@ -78,7 +89,7 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_dma(DmaParams P) {
     uint32_t * act = (uint32_t *) smem;                                 // nb * 32 B
     float * dxp = (float *) (smem + nb * 32);                           // NC * 128 B
     float * sbuf = dxp + NC * 32;                                       // NW * 2 * SPL floats
-    uint8_t * ring0 = (uint8_t *) (sbuf + NW * 2 * SPL);                // NW * R * SLOT
+    uint8_t * ring0 = (uint8_t *) (sbuf + NW * 2 * SPL);                // NW * NC * SLOT
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -182,40 +193,36 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_dma(DmaParams P) {
         return;
     }
 
-    // ---- compute waves: row groups g0 + wave, g0 + wave + NW, ... of this workgroup
+    // ---- compute waves: row group g0 + wave of this workgroup (one per wave: the host
+    // launches NW >= the row groups of any CU), its NC chunks all in flight at once
     const int j = lane & 7;
     const int r = lane >> 3;
     const int nwg = gridDim.x;
     const int g0 = (int) (blockIdx.x * (unsigned) P.G / (unsigned) nwg);     // G * n_cu < 2^32
     const int g1 = (int) ((blockIdx.x + 1) * (unsigned) P.G / (unsigned) nwg);
-    const int ng = max(0, (g1 - g0 - wave + NW - 1) / NW);
     __builtin_amdgcn_s_barrier();               // barrier A: the prologue's input loads went out first
-    if (ng == 0) { lds_barrier(); return; }
-    const int T = ng * NC;                       // chunks of this wave's stream
-    uint8_t * ring = ring0 + (size_t) wave * R * SLOT;
+    if (g0 + wave >= g1) { lds_barrier(); return; }
+    const int grp = g0 + wave;
+    uint8_t * ring = ring0 + (size_t) wave * NC * SLOT;
     const unsigned ring_l = __builtin_amdgcn_readfirstlane(lds_u32(ring));
-    // chunk i (clamped to the last) into ring slot s: 4 nibble sub-chunks + the scales; a
-    // partial last chunk of a row loads its scales again into the unused sub-chunk space,
-    // so every chunk is 5 DMAs
-    auto issue = [&](int i, int s) __attribute__((always_inline)) {
-        i = min(i, T - 1);
-        const int grp = g0 + wave + (i / NC) * NW, cc = i % NC;
+    // chunk cc into slot cc: 4 nibble sub-chunks + the scales; a partial last chunk of a row
+    // loads its scales again into the unused sub-chunk space, so every chunk is 5 DMAs
+    static_for<NC>([&](auto cv) __attribute__((always_inline)) {
+        constexpr int cc = decltype(cv)::value;
         const uint4 * src = P.nib + ((size_t) grp * NC * 4 + cc * 4) * 64 + lane;
         const float4 * ssrc = P.scl + ((size_t) grp * NC + cc) * 64 + lane;
-        const unsigned d = ring_l + (unsigned) s * SLOT;
+        const unsigned d = ring_l + (unsigned) cc * SLOT;
 #pragma unroll
         for (int sb = 0; sb < 4; ++sb) {
-            if (nsub % 4 == 0 || cc * 4 + sb < nsub) dma1k(src + sb * 64, d + sb * 1024);
+            if (cc * 4 + sb < nsub) dma1k(src + sb * 64, d + sb * 1024);
             else dma1k(ssrc, d + sb * 1024);
         }
         dma1k(ssrc, d + 4096);
-    };
-#pragma unroll
-    for (int s = 0; s < R; ++s) issue(s, s);
+    });
 
     float * sw = sbuf + wave * 2 * SPL;
-    auto make_table = [&](int buf, int slot, int cc) __attribute__((always_inline)) {
-        const float4 Sv = *((const float4 *) (ring + (size_t) slot * SLOT + 4096) + lane);
+    auto make_table = [&](int buf, int cc) __attribute__((always_inline)) {
+        const float4 Sv = *((const float4 *) (ring + (size_t) cc * SLOT + 4096) + lane);
         const float4 dx = *(const float4 *) (dxp + cc * 32 + j * 4);
         float4 sv;
         sv.x = Sv.x * dx.x; sv.y = Sv.y * dx.y; sv.z = Sv.z * dx.z; sv.w = Sv.w * dx.w;   // ggml.c:1968
@@ -223,98 +230,86 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_dma(DmaParams P) {
     };
 
     lds_barrier();              // the activation table (dxp) is ready
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(5 * (R - 1)) : "memory");     // chunk 0 landed
-    make_table(0, 0, 0);
+    wait_vm<5 * (NC - 1)>();    // chunk 0 landed (the later chunks may still be in flight)
+    make_table(0, 0);
     __builtin_amdgcn_wave_barrier();
 
-    int tb = 0, slot = 0, i = 0;
-    for (int k = 0; k < ng; ++k) {
-        const int grp = g0 + wave + k * NW;
-        float acc = 0.0f;
+    float acc = 0.0f;
+    static_for<NC>([&](auto cv) __attribute__((always_inline)) {
+        constexpr int c = decltype(cv)::value;
+        constexpr int tb = c & 1;
+        const uint4 * wl = (const uint4 *) (ring + (size_t) c * SLOT) + lane;
+        uint4 W[4];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const uint4 * wl = (const uint4 *) (ring + (size_t) slot * SLOT) + lane;
-            uint4 W[4];
+        for (int sb = 0; sb < 4; ++sb)
+            if (c * 4 + sb < nsub) W[sb] = wl[sb * 64];
+        uint4 A[8];
 #pragma unroll
-            for (int sb = 0; sb < 4; ++sb)
-                if (c * 4 + sb < nsub) W[sb] = wl[sb * 64];
-            uint4 A[8];
+        for (int q = 0; q < 8; ++q)
+            if (c * 4 + q / 2 < nsub) A[q] = *(const uint4 *) (act + ((c * 8 + q) * 8 + j) * 4);
+        const float * sl = sw + tb * SPL;
+        float sa[8][4];
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
-                if (c * 4 + q / 2 < nsub) A[q] = *(const uint4 *) (act + ((c * 8 + q) * 8 + j) * 4);
-            const float * sl = sw + tb * SPL;
-            float sa[8][4];
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-                const float4 v = *(const float4 *) (sl + r * SRS + jj * 4);
-                sa[jj][0] = v.x; sa[jj][1] = v.y; sa[jj][2] = v.z; sa[jj][3] = v.w;
-            }
-            // the slot's reads returned: refill it R chunks ahead (clamped: the count of
-            // DMAs in flight stays 5 per chunk)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            issue(i + R, slot);
-#pragma unroll
-            for (int sb = 0; sb < 4; ++sb) {
-                if (c * 4 + sb < nsub) {
-                    const uint32_t wd[4] = {W[sb].x, W[sb].y, W[sb].z, W[sb].w};
-#pragma unroll
-                    for (int pp = 0; pp < 2; ++pp) {
-                        const int bi = sb * 8 + pp * 4;
-                        const uint4 a = A[sb * 2 + pp];
-                        const int p0 = dot8(wd[2 * pp], a.x);
-                        const int p1 = dot8(wd[2 * pp], a.y);
-                        const int p2 = dot8(wd[2 * pp + 1], a.z);
-                        const int p3 = dot8(wd[2 * pp + 1], a.w);
-                        acc = __builtin_fmaf(sa[(bi + 0) & 7][(bi + 0) >> 3], (float) p0, acc);
-                        acc = __builtin_fmaf(sa[(bi + 1) & 7][(bi + 1) >> 3], (float) p1, acc);
-                        acc = __builtin_fmaf(sa[(bi + 2) & 7][(bi + 2) >> 3], (float) p2, acc);
-                        acc = __builtin_fmaf(sa[(bi + 3) & 7][(bi + 3) >> 3], (float) p3, acc);
-                    }
-                }
-            }
-            ++i;
-            slot = slot + 1 == R ? 0 : slot + 1;
-            // the next chunk's scale table (chunk c+1 of this row group or chunk 0 of the next);
-            // its DMAs have landed once at most the R - 1 chunks after it are in flight
-            if (i < T) {
-                asm volatile("s_waitcnt vmcnt(%0)" :: "n"(5 * (R - 1)) : "memory");
-                make_table(tb ^ 1, slot, c + 1 < NC ? c + 1 : 0);
-            }
-            __builtin_amdgcn_wave_barrier();
-            tb ^= 1;
-            asm volatile("" : "+v"(acc));     // chunks in program order (matvec_cu.hip rule 4)
-            __builtin_amdgcn_sched_barrier(0);
+        for (int jj = 0; jj < 8; ++jj) {
+            const float4 v = *(const float4 *) (sl + r * SRS + jj * 4);
+            sa[jj][0] = v.x; sa[jj][1] = v.y; sa[jj][2] = v.z; sa[jj][3] = v.w;
         }
-        const float res = octet_reduce(acc);
-        const int row = grp * 8 + r;
-        if constexpr (EPI == EPI_STORE) {
-            if (j == 0) P.y[row] = res;
-        } else if constexpr (EPI == EPI_RESID) {
-            if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
-        } else if constexpr (EPI == EPI_QKV) {
-            const int E = P.n_embd, hd = P.head_dim;
-            const int which = row / E;          // 0 q, 1 k, 2 v (uniform per wave: E % 8 == 0)
-            const int e = row - which * E;
-            const int pos = P.sp->n_past;
-            const float other = __shfl_xor(res, 8);   // row e^1 lives in lanes of row r^1
-            if (j == 0) {
-                if (which < 2) {
-                    // ggml_compute_forward_rope_f32 mode 0 (ggml.c:7209-7223)
-                    const int i0 = e % hd;
-                    const float2 cs = P.rope[(size_t) pos * (hd / 2) + (i0 >> 1)];
-                    float out;
-                    if ((i0 & 1) == 0) { const float a = res * cs.x, b = other * cs.y; out = a - b; }
-                    else               { const float a = other * cs.y, b = res * cs.x; out = a + b; }
-                    if (which == 0) kv_store(P.q16, e, out, P.kv32);
-                    else            kv_store(P.kc, (size_t) pos * E + e, out, P.kv32);
-                } else {
-                    kv_store(P.vc, (size_t) e * P.n_ctx + pos, res, P.kv32);     // llama.cpp:996-1008
+#pragma unroll
+        for (int sb = 0; sb < 4; ++sb) {
+            if (c * 4 + sb < nsub) {
+                const uint32_t wd[4] = {W[sb].x, W[sb].y, W[sb].z, W[sb].w};
+#pragma unroll
+                for (int pp = 0; pp < 2; ++pp) {
+                    const int bi = sb * 8 + pp * 4;
+                    const uint4 a = A[sb * 2 + pp];
+                    const int p0 = dot8(wd[2 * pp], a.x);
+                    const int p1 = dot8(wd[2 * pp], a.y);
+                    const int p2 = dot8(wd[2 * pp + 1], a.z);
+                    const int p3 = dot8(wd[2 * pp + 1], a.w);
+                    acc = __builtin_fmaf(sa[(bi + 0) & 7][(bi + 0) >> 3], (float) p0, acc);
+                    acc = __builtin_fmaf(sa[(bi + 1) & 7][(bi + 1) >> 3], (float) p1, acc);
+                    acc = __builtin_fmaf(sa[(bi + 2) & 7][(bi + 2) >> 3], (float) p2, acc);
+                    acc = __builtin_fmaf(sa[(bi + 3) & 7][(bi + 3) >> 3], (float) p3, acc);
                 }
+            }
+        }
+        // the next chunk's scale table; its DMAs landed once the NC - 2 - c after it may
+        // still be in flight
+        if constexpr (c + 1 < NC) {
+            wait_vm<5 * (NC - 2 - c)>();
+            make_table(tb ^ 1, c + 1);
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" : "+v"(acc));     // chunks in program order (matvec_cu.hip rule 4)
+        __builtin_amdgcn_sched_barrier(0);
+    });
+    const float res = octet_reduce(acc);
+    const int row = grp * 8 + r;
+    if constexpr (EPI == EPI_STORE) {
+        if (j == 0) P.y[row] = res;
+    } else if constexpr (EPI == EPI_RESID) {
+        if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+    } else if constexpr (EPI == EPI_QKV) {
+        const int E = P.n_embd, hd = P.head_dim;
+        const int which = row / E;          // 0 q, 1 k, 2 v (uniform per wave: E % 8 == 0)
+        const int e = row - which * E;
+        const int pos = P.sp->n_past;
+        const float other = __shfl_xor(res, 8);   // row e^1 lives in lanes of row r^1
+        if (j == 0) {
+            if (which < 2) {
+                // ggml_compute_forward_rope_f32 mode 0 (ggml.c:7209-7223)
+                const int i0 = e % hd;
+                const float2 cs = P.rope[(size_t) pos * (hd / 2) + (i0 >> 1)];
+                float out;
+                if ((i0 & 1) == 0) { const float a = res * cs.x, b = other * cs.y; out = a - b; }
+                else               { const float a = other * cs.y, b = res * cs.x; out = a + b; }
+                if (which == 0) kv_store(P.q16, e, out, P.kv32);
+                else            kv_store(P.kc, (size_t) pos * E + e, out, P.kv32);
+            } else {
+                kv_store(P.vc, (size_t) e * P.n_ctx + pos, res, P.kv32);     // llama.cpp:996-1008
             }
         }
     }
-    // the clamped refills must land before the workgroup's LDS is released
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---- Q4_1 (13B): the k_mv_cu41 chains (ggml_vec_dot_q4_1 AVX2, ggml.c:2188-2258) with
@@ -407,139 +402,134 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_dma41(Dma41Params P) {
         return;
     }
 
+    // one row group per compute wave (the host launches NW >= the row groups of any CU);
+    // its chunks stream through a ring of R slots, chunk c in slot c % R
     const int j = lane & 7;
     const int r = lane >> 3;
     const int nwg = gridDim.x;
     const int g0 = (int) (blockIdx.x * (unsigned) P.G / (unsigned) nwg);
     const int g1 = (int) ((blockIdx.x + 1) * (unsigned) P.G / (unsigned) nwg);
-    const int ng = max(0, (g1 - g0 - wave + NW - 1) / NW);
     __builtin_amdgcn_s_barrier();               // barrier A
-    if (ng == 0) { lds_barrier(); return; }
-    const int T = ng * NC;
+    if (g0 + wave >= g1) { lds_barrier(); return; }
+    const int grp = g0 + wave;
     uint8_t * ring = ring0 + (size_t) wave * R * SLOT41;
     const unsigned ring_l = __builtin_amdgcn_readfirstlane(lds_u32(ring));
-    // chunk i (clamped) into slot s: 4 nibble sub-chunks (filler past a row's end), d, m, wsum
-    auto issue = [&](int i, int s) __attribute__((always_inline)) {
-        i = min(i, T - 1);
-        const int grp = g0 + wave + (i / NC) * NW, cc = i % NC;
+    // chunk cc into its slot: 4 nibble sub-chunks (filler past a row's end), d, m, wsum
+    auto issue = [&](auto cv) __attribute__((always_inline)) {
+        constexpr int cc = decltype(cv)::value;
         const uint4 * src = P.nib + ((size_t) grp * NC * 4 + cc * 4) * 64 + lane;
         const float4 * ssrc = P.scl + ((size_t) grp * NC + cc) * 128 + lane;
         const uint4 * wsrc = P.wsum + ((size_t) grp * NC + cc) * 64 + lane;
-        const unsigned d = ring_l + (unsigned) s * SLOT41;
+        const unsigned d = ring_l + (unsigned) (cc % R) * SLOT41;
 #pragma unroll
         for (int sb = 0; sb < 4; ++sb) {
-            if (nsub % 4 == 0 || cc * 4 + sb < nsub) dma1k(src + sb * 64, d + sb * 1024);
+            if (cc * 4 + sb < nsub) dma1k(src + sb * 64, d + sb * 1024);
             else dma1k(wsrc, d + sb * 1024);
         }
         dma1k(ssrc, d + 4096);
         dma1k(ssrc + 64, d + 5120);
         dma1k(wsrc, d + 6144);
     };
-#pragma unroll
-    for (int s = 0; s < R; ++s) issue(s, s);
+    static_for<(R < NC ? R : NC)>(issue);
 
     lds_barrier();              // the activation table is ready
     const bool even = (j & 1) == 0;
     const uint32_t * ys32 = (const uint32_t *) ys;
     float * sw = sbuf + wave * SWF41;
-    int slot = 0, i = 0;
-    for (int k = 0; k < ng; ++k) {
-        const int grp = g0 + wave + k * NW;
-        float acc = 0.0f, off = 0.0f;
+    float acc = 0.0f, off = 0.0f;
+    static_for<NC>([&](auto cv) __attribute__((always_inline)) {
+        constexpr int c = decltype(cv)::value;
+        // chunk c landed once at most the chunks issued after it are in flight
+        wait_vm<7 * ((c + R - 1 < NC - 1 ? c + R - 1 : NC - 1) - c)>();
+        const uint4 * wl = (const uint4 *) (ring + (size_t) (c % R) * SLOT41) + lane;
+        uint4 W[4];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            // chunk i landed once at most the R - 1 chunks after it are in flight
-            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(7 * (R - 1)) : "memory");
-            const uint4 * wl = (const uint4 *) (ring + (size_t) slot * SLOT41) + lane;
-            uint4 W[4];
+        for (int sb = 0; sb < 4; ++sb)
+            if (c * 4 + sb < nsub) W[sb] = wl[sb * 64];
+        const float4 SD = *(const float4 *) (wl + 256);
+        const float4 SM = *(const float4 *) (wl + 320);
+        const uint4 WS = wl[384];
+        // products of blocks 32c + 8m + j of this lane's row (ggml.c:2205-2212)
+        const float4 dy = *(const float4 *) (dyv + c * 32 + j * 4);
+        const float4 my = *(const float4 *) (myv + c * 32 + j * 4);
+        float * sl = sw + r * SRS + j;
+        const float dxa[4] = {SD.x, SD.y, SD.z, SD.w};
+        const float mxa[4] = {SM.x, SM.y, SM.z, SM.w};
+        const float dya[4] = {dy.x, dy.y, dy.z, dy.w};
+        const float mya[4] = {my.x, my.y, my.z, my.w};
 #pragma unroll
-            for (int sb = 0; sb < 4; ++sb)
-                if (c * 4 + sb < nsub) W[sb] = wl[sb * 64];
-            const float4 SD = *(const float4 *) (wl + 256);
-            const float4 SM = *(const float4 *) (wl + 320);
-            const uint4 WS = wl[384];
-            // products of blocks 32c + 8m + j of this lane's row (ggml.c:2205-2212)
-            const float4 dy = *(const float4 *) (dyv + c * 32 + j * 4);
-            const float4 my = *(const float4 *) (myv + c * 32 + j * 4);
-            float * sl = sw + r * SRS + j;
-            const float dxa[4] = {SD.x, SD.y, SD.z, SD.w};
-            const float mxa[4] = {SM.x, SM.y, SM.z, SM.w};
-            const float dya[4] = {dy.x, dy.y, dy.z, dy.w};
-            const float mya[4] = {my.x, my.y, my.z, my.w};
-#pragma unroll
-            for (int mq = 0; mq < 4; ++mq) {
-                sl[mq * 8] = dxa[mq] * dya[mq];
-                sl[SPL + mq * 8] = dxa[mq] * mya[mq];
-                sl[2 * SPL + mq * 8] = mxa[mq] * dya[mq];
-                sl[3 * SPL + mq * 8] = mxa[mq] * mya[mq];
-            }
-            // the slot's operands are in registers: refill it R chunks ahead (clamped)
+        for (int mq = 0; mq < 4; ++mq) {
+            sl[mq * 8] = dxa[mq] * dya[mq];
+            sl[SPL + mq * 8] = dxa[mq] * mya[mq];
+            sl[2 * SPL + mq * 8] = mxa[mq] * dya[mq];
+            sl[3 * SPL + mq * 8] = mxa[mq] * mya[mq];
+        }
+        // the slot's operands are in registers: refill it with chunk c + R
+        if constexpr (c + R < NC) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            issue(i + R, slot);
-            __builtin_amdgcn_wave_barrier();
-            const float * srow = sw + r * SRS;
-            const float * xrow = srow + (even ? SPL : 2 * SPL);
-            const float * mrow = srow + 3 * SPL;
-            // even chains: the precomputed weight sums (blocks 0-15 of the chunk in their own
-            // word, 16-31 in the odd neighbour's: DPP quad_perm [1,1,3,3]); odd chains: the
-            // activation sums from LDS (ggml.c:2236-2240), one byte per block
-            const uint32_t wown[4] = {WS.x, WS.y, WS.z, WS.w};
-            uint32_t wnb[4];
+            issue(std::integral_constant<int, c + R>{});
+        }
+        __builtin_amdgcn_wave_barrier();
+        const float * srow = sw + r * SRS;
+        const float * xrow = srow + (even ? SPL : 2 * SPL);
+        const float * mrow = srow + 3 * SPL;
+        // even chains: the precomputed weight sums (blocks 0-15 of the chunk in their own
+        // word, 16-31 in the odd neighbour's: DPP quad_perm [1,1,3,3]); odd chains: the
+        // activation sums from LDS (ggml.c:2236-2240), one byte per block
+        const uint32_t wown[4] = {WS.x, WS.y, WS.z, WS.w};
+        uint32_t wnb[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) wnb[q] = (uint32_t) __builtin_amdgcn_mov_dpp((int) wown[q], 0xF5, 0xF, 0xF, false);
+        for (int q = 0; q < 4; ++q) wnb[q] = (uint32_t) __builtin_amdgcn_mov_dpp((int) wown[q], 0xF5, 0xF, 0xF, false);
 #pragma unroll
-            for (int sb = 0; sb < 4; ++sb) {
-                if (c * 4 + sb < nsub) {
-                    const uint32_t wd[4] = {W[sb].x, W[sb].y, W[sb].z, W[sb].w};
+        for (int sb = 0; sb < 4; ++sb) {
+            if (c * 4 + sb < nsub) {
+                const uint32_t wd[4] = {W[sb].x, W[sb].y, W[sb].z, W[sb].w};
 #pragma unroll
-                    for (int pp = 0; pp < 2; ++pp) {
-                        const int uu = c * 8 + sb * 2 + pp;
-                        const int bi = sb * 8 + pp * 4;
-                        const uint4 a = *(const uint4 *) (act + ((size_t) uu * 8 + j) * 4);
-                        const float4 s4 = *(const float4 *) (srow + bi);
-                        const float4 x4 = *(const float4 *) (xrow + bi);
-                        const float4 m4 = *(const float4 *) (mrow + bi);
-                        const uint32_t ydw = ys32[(size_t) uu * 4 + (j >> 1)];
-                        const uint32_t wdw = sb < 2 ? wown[(sb & 1) * 2 + pp] : wnb[(sb & 1) * 2 + pp];
-                        const uint32_t sdw = even ? wdw : ydw;
-                        const float S[4] = {(float) (sdw & 0xFFu), (float) ((sdw >> 8) & 0xFFu),
-                                            (float) ((sdw >> 16) & 0xFFu), (float) (sdw >> 24)};
-                        const int p[4] = {udot8(wd[2 * pp], a.x), udot8(wd[2 * pp], a.y),
-                                          udot8(wd[2 * pp + 1], a.z), udot8(wd[2 * pp + 1], a.w)};
-                        const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
-                        const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
-                        const float ms[4] = {m4.x, m4.y, m4.z, m4.w};
+                for (int pp = 0; pp < 2; ++pp) {
+                    const int uu = c * 8 + sb * 2 + pp;
+                    const int bi = sb * 8 + pp * 4;
+                    const uint4 a = *(const uint4 *) (act + ((size_t) uu * 8 + j) * 4);
+                    const float4 s4 = *(const float4 *) (srow + bi);
+                    const float4 x4 = *(const float4 *) (xrow + bi);
+                    const float4 m4 = *(const float4 *) (mrow + bi);
+                    const uint32_t ydw = ys32[(size_t) uu * 4 + (j >> 1)];
+                    const uint32_t wdw = sb < 2 ? wown[(sb & 1) * 2 + pp] : wnb[(sb & 1) * 2 + pp];
+                    const uint32_t sdw = even ? wdw : ydw;
+                    const float S[4] = {(float) (sdw & 0xFFu), (float) ((sdw >> 8) & 0xFFu),
+                                        (float) ((sdw >> 16) & 0xFFu), (float) (sdw >> 24)};
+                    const int p[4] = {udot8(wd[2 * pp], a.x), udot8(wd[2 * pp], a.y),
+                                      udot8(wd[2 * pp + 1], a.z), udot8(wd[2 * pp + 1], a.w)};
+                    const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+                    const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+                    const float ms[4] = {m4.x, m4.y, m4.z, m4.w};
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            acc = __builtin_fmaf(sv[q], (float) p[q], acc);    // ggml.c:2244
-                            acc = __builtin_fmaf(xs[q], S[q], acc);            // ggml.c:2247
-                            off = off + ms[q];                                 // ggml.c:2226
-                        }
+                    for (int q = 0; q < 4; ++q) {
+                        acc = __builtin_fmaf(sv[q], (float) p[q], acc);    // ggml.c:2244
+                        acc = __builtin_fmaf(xs[q], S[q], acc);            // ggml.c:2247
+                        off = off + ms[q];                                 // ggml.c:2226
                     }
                 }
             }
-            ++i;
-            slot = slot + 1 == R ? 0 : slot + 1;
-            // the product tables are rewritten by the next chunk
-            asm volatile("" : "+v"(acc), "+v"(off));
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_sched_barrier(0);
         }
-        const float res = octet_reduce(acc) + off * 32.0f;      // acc_offset * QK (ggml.c:2249)
-        const int row = grp * 8 + r;
-        if constexpr (EPI == EPI_STORE) {
-            if (j == 0) P.y[row] = res;
-        } else {
-            if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
-        }
+        // the product tables are rewritten by the next chunk
+        asm volatile("" : "+v"(acc), "+v"(off));
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    });
+    const float res = octet_reduce(acc) + off * 32.0f;      // acc_offset * QK (ggml.c:2249)
+    const int row = grp * 8 + r;
+    if constexpr (EPI == EPI_STORE) {
+        if (j == 0) P.y[row] = res;
+    } else {
+        if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <int NW, int NP, int R, int PRO, int EPI, int KT>
 hipError_t go41(const Dma41Params & P, hipStream_t s) {
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
     const int nwg = std::min(cu_count(), P.G);
+    if ((P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;      // one row group per wave
     const size_t lds = (size_t) nb * 32 + 2 * NC * 128 + (size_t) nb * 16 + (size_t) NW * SWF41 * 4 +
                        (size_t) NW * R * SLOT41;
     if (lds > 160 * 1024) return hipErrorNotSupported;
@@ -550,8 +540,10 @@ hipError_t go41(const Dma41Params & P, hipStream_t s) {
 template <int NW, int NP, int R, int PRO, int EPI, int KT>
 hipError_t go(const DmaParams & P, hipStream_t s) {
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
+    static_assert(R == NC, "the Q4_0 form keeps a whole row group in flight");
     const int nwg = std::min(cu_count(), P.G);
-    const size_t lds = (size_t) nb * 32 + NC * 128 + (size_t) NW * 2 * SPL * 4 + (size_t) NW * R * SLOT;
+    if ((P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;      // one row group per wave
+    const size_t lds = (size_t) nb * 32 + NC * 128 + (size_t) NW * 2 * SPL * 4 + (size_t) NW * NC * SLOT;
     if (lds > 160 * 1024) return hipErrorNotSupported;
     LVK_LAUNCH((k_mv_dma<NW, NP, R, PRO, EPI, KT>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
     return hipGetLastError();

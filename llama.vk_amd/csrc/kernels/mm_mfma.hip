@@ -43,6 +43,8 @@
 #include "lvk_kernels.h"
 #include "matvec_common.h"
 
+#include <cstdlib>
+
 namespace lvk {
 
 namespace {
@@ -96,6 +98,8 @@ struct MmParams {
     int ldy;
     int out_tok0;
     const uint16_t * silu_tab;
+    int variant;             // LVK_MM_VARIANT (A/B runs): 1 s_setprio 1 on odd workgroups, 2 odd
+                             // workgroups start half a block late, 4 super tiles of 4 row tiles
 };
 
 __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t o) {
@@ -142,8 +146,16 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
     const int bid = blockIdx.x;
     const int full = nwg & ~7;
     const int L = bid < full ? (bid & 7) * (full >> 3) + (bid >> 3) : bid;
-    const int tt = L % P.ntt;
-    const int m0 = (L / P.ntt) * TM;
+    int tt = L % P.ntt, rt = L / P.ntt;
+    if (P.variant & 4) {
+        // super tiles of 4 row tiles x all token tiles, token tiles outer: the 64 workgroups
+        // an XCD runs at once share 4 weight tiles and 16 activation tiles in its L2
+        const int nrt = P.M / TM, per = 4 * P.ntt, sidx = L / per, wi = L % per;
+        if (4 * sidx + 3 < nrt) { tt = wi >> 2; rt = 4 * sidx + (wi & 3); }
+    }
+    if ((P.variant & 1) && (bid & 1)) __builtin_amdgcn_s_setprio(1);
+    if ((P.variant & 2) && (bid & 1)) __builtin_amdgcn_s_sleep(3);
+    const int m0 = rt * TM;
     const int n0 = tt * TN;
     const int nb = P.nb, NC = P.NC;
     const int G0 = m0 / 8;
@@ -552,6 +564,8 @@ hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, 
     P.xm = (const uint2 *) xm; P.da = da; P.N = N; P.ntt = (N + TN - 1) / TN;
     P.y = y; P.ldy = ldy; P.out_tok0 = out_tok0; P.silu_tab = silu_tab;
     P.a16 = (const uint2 *) w.a16;
+    static const int variant = [] { const char * e = getenv("LVK_MM_VARIANT"); return e ? atoi(e) : 0; }();
+    P.variant = variant;
     const dim3 grid((w.M / TM) * P.ntt);
 #define LVK_MM_GO(E)                                                                      \
     do {                                                                                  \
