@@ -143,4 +143,18 @@ __device__ __forceinline__ size_t xm_slot(int t, int nb, int b, int c, int l) {
     return ((((size_t) (t >> 4) * nb + b) * 2 + (c >> 1)) * 64 + l) * 2 + (c & 1);
 }
 
+// prompt-matmul tile of workgroup slot L (its XCD-contiguous index, mm_mfma.hip): row tile
+// rt, token tile tt.  Row tiles outer, token tiles inner; supertile: groups of 4 row tiles x
+// every token tile with the token tiles outer, so the 64 workgroups an XCD runs at once share
+// 4 weight tiles and 16 activation tiles in its L2 instead of 2 weight tiles and the whole
+// activation image (7B 512-token prompt 45.3 -> 43.7 ms, profiles/r04_prompt_variants.jsonl)
+__device__ __forceinline__ void mm_tile(int L, int ntt, int nrt, int supertile, int & rt, int & tt) {
+    tt = L % ntt;
+    rt = L / ntt;
+    if (supertile) {
+        const int per = 4 * ntt, sidx = L / per, wi = L % per;
+        if (4 * sidx + 3 < nrt) { tt = wi >> 2; rt = 4 * sidx + (wi & 3); }
+    }
+}
+
 }  // namespace lvk

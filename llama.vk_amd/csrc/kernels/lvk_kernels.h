@@ -130,10 +130,6 @@ hipError_t launch_matvec_q41(const MvLaunch & L, int pro, int epi, hipStream_t s
 bool matvec_cu_supported(int K, int qtype = Q4_0);
 hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s);
 bool matvec_cu41_supported(int K);
-// the Q4_0 decode matvec with its weights streamed into LDS by LDS-DMA (matvec_dma.hip):
-// Wo / W2 shapes with at most two row groups per CU; hipErrorNotSupported otherwise
-bool matvec_dma_enabled();
-hipError_t launch_matvec_dma(const MvLaunch & L, int pro, int epi, hipStream_t s);
 hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t s);
 // compute units of the current device (one decode workgroup per CU)
 int cu_count();
@@ -214,6 +210,9 @@ inline const uint4 * q41_wsum(const QMatrix & w) {
 // launch_actq_to_f16.  epi: EPI_STORE, EPI_RESID (y += W x), EPI_SWIGLU_F32
 // (fused W1|W3 image -> u = silu(w1 x) * (w3 x)).
 bool mm_mfma_supported(const QMatrix & w);
+// prompt-matmul tile order: 1 = super tiles of 4 row tiles (default), 0 = row tiles
+// (LVK_MM_SUPERTILE; device/lvk_device.h mm_tile)
+int mm_supertile();
 size_t mm_act_bytes(int N, int K);
 // the f16 A-fragment image of a Q4_0 matrix (QMatrix::a16): bytes, and its build from the
 // matrix's octet image (M % 32 == 0)

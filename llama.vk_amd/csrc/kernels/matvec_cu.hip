@@ -551,12 +551,6 @@ bool matvec_cu_supported(int K, int qtype) {
 hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s) {
     if (L.w.qtype == Q4_1) return launch_matvec_cu41(L, pro, epi, s);
     if (L.w.qtype != Q4_0 || L.n_tokens != 1 || L.w.M % 8) return hipErrorNotSupported;
-    // Wo / W2 (two row groups per CU): the LDS-DMA form puts the whole launch's weights in
-    // flight at once (matvec_dma.hip)
-    if ((epi == EPI_RESID || epi == EPI_QKV) && matvec_dma_enabled()) {
-        const hipError_t e = launch_matvec_dma(L, pro, epi, s);
-        if (e != hipErrorNotSupported) return e;
-    }
     CuParams P{};
     P.nib = L.w.nib;
     P.scl = (const float4 *) L.w.scl;

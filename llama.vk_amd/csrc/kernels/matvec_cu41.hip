@@ -351,11 +351,6 @@ bool matvec_cu41_supported(int K) { return K == 4096 || K == 5120 || K == 11008 
 
 hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t s) {
     if (L.w.qtype != Q4_1 || L.n_tokens != 1 || L.w.M % 8) return hipErrorNotSupported;
-    // Wo / W2 (2-3 row groups per CU): the LDS-DMA form (matvec_dma.hip)
-    if (epi == EPI_RESID && matvec_dma_enabled()) {
-        const hipError_t e = launch_matvec_dma(L, pro, epi, s);
-        if (e != hipErrorNotSupported) return e;
-    }
     Cu41Params P{};
     P.nib = L.w.nib;
     P.scl = (const float4 *) L.w.scl;

@@ -98,8 +98,7 @@ struct MmParams {
     int ldy;
     int out_tok0;
     const uint16_t * silu_tab;
-    int variant;             // LVK_MM_VARIANT (A/B runs): 1 s_setprio 1 on odd workgroups, 2 odd
-                             // workgroups start half a block late, 4 super tiles of 4 row tiles
+    int supertile;           // 1: super tiles of 4 row tiles (default; LVK_MM_SUPERTILE=0: row tiles)
 };
 
 __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t o) {
@@ -146,15 +145,8 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
     const int bid = blockIdx.x;
     const int full = nwg & ~7;
     const int L = bid < full ? (bid & 7) * (full >> 3) + (bid >> 3) : bid;
-    int tt = L % P.ntt, rt = L / P.ntt;
-    if (P.variant & 4) {
-        // super tiles of 4 row tiles x all token tiles, token tiles outer: the 64 workgroups
-        // an XCD runs at once share 4 weight tiles and 16 activation tiles in its L2
-        const int nrt = P.M / TM, per = 4 * P.ntt, sidx = L / per, wi = L % per;
-        if (4 * sidx + 3 < nrt) { tt = wi >> 2; rt = 4 * sidx + (wi & 3); }
-    }
-    if ((P.variant & 1) && (bid & 1)) __builtin_amdgcn_s_setprio(1);
-    if ((P.variant & 2) && (bid & 1)) __builtin_amdgcn_s_sleep(3);
+    int tt, rt;
+    mm_tile(L, P.ntt, P.M / TM, P.supertile, rt, tt);
     const int m0 = rt * TM;
     const int n0 = tt * TN;
     const int nb = P.nb, NC = P.NC;
@@ -215,7 +207,7 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
     auto load_aq = [&](int blk, uint2 (&q)[4]) {
 #pragma unroll
         for (int c2 = 0; c2 < 2; ++c2) {
-            const uint4 v = a16p[(size_t) blk * 128 + c2 * 64];
+            const uint4 v = (LVK_MM_EXP & 8) ? make_uint4(blk, c2, 7, 1) : a16p[(size_t) blk * 128 + c2 * 64];
             q[2 * c2] = make_uint2(v.x, v.y);
             q[2 * c2 + 1] = make_uint2(v.z, v.w);
         }
@@ -539,6 +531,11 @@ __global__ void k_a16_from_octet(const uint4 * __restrict__ nib, int M, int K, u
 
 }  // namespace
 
+int mm_supertile() {
+    static const int v = [] { const char * e = getenv("LVK_MM_SUPERTILE"); return e ? atoi(e) : 1; }();
+    return v;
+}
+
 size_t mm_a16_bytes(int M, int K) { return (size_t) (M / 32) * (K / 32) * 256 * 8; }
 
 hipError_t launch_build_a16(const QMatrix & w, void * a16, hipStream_t s) {
@@ -564,8 +561,7 @@ hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, 
     P.xm = (const uint2 *) xm; P.da = da; P.N = N; P.ntt = (N + TN - 1) / TN;
     P.y = y; P.ldy = ldy; P.out_tok0 = out_tok0; P.silu_tab = silu_tab;
     P.a16 = (const uint2 *) w.a16;
-    static const int variant = [] { const char * e = getenv("LVK_MM_VARIANT"); return e ? atoi(e) : 0; }();
-    P.variant = variant;
+    P.supertile = mm_supertile();
     const dim3 grid((w.M / TM) * P.ntt);
 #define LVK_MM_GO(E)                                                                      \
     do {                                                                                  \

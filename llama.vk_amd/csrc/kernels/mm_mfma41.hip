@@ -63,6 +63,7 @@ struct Mm41Params {
     float * y;
     int ldy;
     const uint16_t * silu_tab;
+    int supertile;           // mm_tile order (mm_mfma.hip)
 };
 
 struct Blk {                 // one block's operands of one lane
@@ -127,8 +128,9 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q41_mfma(Mm41Params P) {
     const int bid = blockIdx.x;
     const int full = nwg & ~7;
     const int L = bid < full ? (bid & 7) * (full >> 3) + (bid >> 3) : bid;
-    const int tt = L % P.ntt;
-    const int m0 = (L / P.ntt) * TM;
+    int tt, rtile;
+    mm_tile(L, P.ntt, P.M / TM, P.supertile, rtile, tt);
+    const int m0 = rtile * TM;
     const int n0 = tt * TN;
     const int nb = P.nb;
     const int rt = m0 / 32 + w;                              // this wave's 32-row tile
@@ -244,8 +246,9 @@ __global__ __launch_bounds__(NT, OCC41) void k_mm_q41_dma(Mm41Params P) {
     const int bid = blockIdx.x;
     const int full = nwg & ~7;
     const int L = bid < full ? (bid & 7) * (full >> 3) + (bid >> 3) : bid;
-    const int tt = L % P.ntt;
-    const int m0 = (L / P.ntt) * TM;
+    int tt, rtile;
+    mm_tile(L, P.ntt, P.M / TM, P.supertile, rtile, tt);
+    const int m0 = rtile * TM;
     const int n0 = tt * TN;
     const int nb = P.nb;
     const int rt = m0 / 32 + w;
@@ -488,6 +491,7 @@ hipError_t launch_mm_mfma41(const QMatrix & w, const void * xm, const void * xs,
     P.xm = (const uint4 *) xm; P.xs = (const uint4 *) xs;
     P.M = w.M; P.nb = w.K / 32; P.N = N; P.ntt = (N + TN - 1) / TN;
     P.y = y; P.ldy = ldy; P.silu_tab = silu_tab;
+    P.supertile = mm_supertile();
     const dim3 grid((w.M / TM) * P.ntt);
     // LVK_MM41_DMA=0: the register-ring kernel instead of the LDS-DMA ring
     const char * dma_env = getenv("LVK_MM41_DMA");

@@ -25,9 +25,6 @@ def klass(name):
     m = re.search(r"k_mv_cu<(\d+), (\d+), (\d+), (\d+), (\d+), (\d+)", name)
     if m:                                   # <NW, NP, D, PRO, EPI, KT, PF>
         epi, kt = int(m.group(5)), int(m.group(6))
-    elif re.search(r"k_mv_dma<", name):     # <NW, NP, R, PRO, EPI, KT>
-        m = re.search(r"k_mv_dma<(\d+), (\d+), (\d+), (\d+), (\d+), (\d+)", name)
-        epi, kt = int(m.group(5)), int(m.group(6))
     else:
         m = re.search(r"k_mv_cu41<(\d+), (\d+), (\d+), (\d+), (\d+)", name)
         if not m:

@@ -41,6 +41,12 @@ int main(int argc, char ** argv) {
         hipLaunchKernelGGL(k_fill_u32, dim3(1024), dim3(256), 0, 0, (uint32_t *) nib, qimage_nib_bytes(s.M, s.K) / 4, 7u);
         hipLaunchKernelGGL(k_fill_f32, dim3(1024), dim3(256), 0, 0, (float *) scl, qimage_scl_bytes(s.M, s.K) / 4, 0.001f, 0.01f, 9u);
         q.nib = (const uint4 *) nib; q.scl = scl;
+        void * a16 = nullptr;
+        if (getenv("MM_A16") && atoi(getenv("MM_A16"))) {       // the product's f16 A image
+            a16 = dalloc(mm_a16_bytes(s.M, s.K));
+            CK(launch_build_a16(q, a16, 0));
+            q.a16 = a16;
+        }
         CK(launch_act_f16(x, nullptr, N, s.K, xh, da, 0));
         for (int i = 0; i < 2; ++i) CK(launch_mm_mfma(q, xh, da, N, y, s.M, 0, s.epi, stab, 0));
         CK(hipDeviceSynchronize());
@@ -54,6 +60,7 @@ int main(int argc, char ** argv) {
                partials / us * 1e-6, (double) s.M * N * s.K / us * 1e-6);
         total += us;
         CK(hipFree(nib)); CK(hipFree(scl));
+        if (a16) CK(hipFree(a16));
     }
     printf("layer total %.1f us -> 32 layers %.2f ms\n", total, total * 32 / 1e3);
     return 0;
