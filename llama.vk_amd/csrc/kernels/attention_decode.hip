@@ -169,6 +169,8 @@ struct AttnDArgs {
     unsigned * err;               // host-mapped error word (nullptr: none)
     int short_max;                // n_kv <= short_max: no score exchange (every workgroup scores all)
     int seq_epochs;               // epoch += sp->seq << 7 (granules never zeroed between tokens)
+    int vorder;                   // V chunk-0 DMA (LVK_ATTN_VORDER, A/B): 0 before the n_past-dependent
+                                  // K loads, 1 after them, 2 with the rest of V behind the first scores
 };
 
 // The 4 workgroups of a head either split the scores and exchange them as granules, or
@@ -221,7 +223,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
 #pragma unroll
         for (int st = 0; st < 4; ++st) kv[0][st] = kp[st * 4];
     }
-    v_dma(0, 0, 64);
+    if (A.vorder == 0) v_dma(0, 0, 64);
     const int n_kv = n_past + 1;
     const int n_pad = (n_kv + 31) & ~31;
     const int np = n_kv & ~31;
@@ -243,6 +245,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
 #pragma unroll
         for (int st = 0; st < 4; ++st) kv[1][st] = kp[st * 4];
     }
+    if (A.vorder == 1) v_dma(0, 0, 64);
     LVK_DT(6);
 
     // 1b. scores of chunks sl, sl+4, ... (exchange) or of every chunk (one position per lane quad)
@@ -277,7 +280,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
         if (cb + cs < n_kv) score(kv[1], cb + cs + (tid >> 2));
         // the rest of the V slice goes out behind the first two chunks' scores: those wait
         // only for their own K rows, the V rows are needed after the softmax
-        for (int p0 = 0; p0 < n_pad; p0 += 512) v_dma(p0, 64, n_pad);
+        for (int p0 = 0; p0 < n_pad; p0 += 512) v_dma(p0, A.vorder == 2 ? 0 : 64, n_pad);
         LVK_DT(7);
         LVK_DT(1);
         for (int c0 = cb + 2 * cs; c0 < n_kv; c0 += cs) {
@@ -709,6 +712,8 @@ AttnDArgs attn_args(const AttnLaunch & A, void * gran, unsigned epoch) {
     }();
     a.short_max = short_max;
     a.seq_epochs = A.seq_epochs;
+    static const int vorder = [] { const char * e = getenv("LVK_ATTN_VORDER"); return e ? atoi(e) : 0; }();
+    a.vorder = vorder;
     return a;
 }
 

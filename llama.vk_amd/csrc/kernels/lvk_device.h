@@ -147,13 +147,15 @@ __device__ __forceinline__ size_t xm_slot(int t, int nb, int b, int c, int l) {
 // rt, token tile tt.  Row tiles outer, token tiles inner; supertile: groups of 4 row tiles x
 // every token tile with the token tiles outer, so the 64 workgroups an XCD runs at once share
 // 4 weight tiles and 16 activation tiles in its L2 instead of 2 weight tiles and the whole
-// activation image (7B 512-token prompt 45.3 -> 43.7 ms, profiles/r04_prompt_variants.jsonl)
+// activation image (7B 512-token prompt 45.3 -> 43.7 ms, profiles/r04_prompt_variants.jsonl);
+// LVK_MM_SUPERTILE = R > 1 sets the group width (A/B)
 __device__ __forceinline__ void mm_tile(int L, int ntt, int nrt, int supertile, int & rt, int & tt) {
     tt = L % ntt;
     rt = L / ntt;
-    if (supertile) {
-        const int per = 4 * ntt, sidx = L / per, wi = L % per;
-        if (4 * sidx + 3 < nrt) { tt = wi >> 2; rt = 4 * sidx + (wi & 3); }
+    const int R = supertile == 1 ? 4 : supertile;     // row tiles per super tile (1: the default 4)
+    if (R > 1) {
+        const int per = R * ntt, sidx = L / per, wi = L % per;
+        if (R * sidx + R - 1 < nrt) { tt = wi / R; rt = R * sidx + wi % R; }
     }
 }
 

@@ -58,7 +58,7 @@ constexpr int TM = 128;     // rows per workgroup
 constexpr int TN = 16;      // tokens per workgroup (one token tile)
 constexpr int NT = 256;     // threads (4 waves)
 // LVK_MM_EXP (dev probe builds only, tools/probe), bit flags: 1 no fp32 chains, 2 no MFMA, 4 no B loads,
-// 8 no A loads
+// 8 no A loads, 16 / 32 L2-hot A / B (below)
 #ifndef LVK_MM_EXP
 #define LVK_MM_EXP 0
 #endif
@@ -84,6 +84,14 @@ constexpr int LDS_DA = (32 * DAS * 4 + 15) / 16 * 16;   // [block of chunk][toke
 constexpr int OFF_DW0 = 0, OFF_DW1 = LDS_DW;
 constexpr int OFF_DA0 = 2 * LDS_DW, OFF_DA1 = OFF_DA0 + LDS_DA;
 constexpr int LDS_TOTAL = OFF_DA1 + LDS_DA;         // ~37 KiB
+// A16 + LVK_MM_BLDS: the token tile's B fragments of one sub-chunk (8 blocks x 2 x 64 lanes x
+// 16 B) staged once per workgroup in LDS, double-buffered, instead of each wave loading them
+#ifndef LVK_MM_BLDS
+#define LVK_MM_BLDS 1
+#endif
+constexpr int LDS_BSUB = 8 * 128 * 16;               // 16 KiB per sub-chunk
+constexpr int OFF_B0 = LDS_TOTAL, OFF_B1 = OFF_B0 + LDS_BSUB;
+constexpr int LDS_TOTAL_BL = OFF_B1 + LDS_BSUB;     // ~69 KiB: two workgroups per CU
 
 struct MmParams {
     const uint4 * nib;
@@ -128,6 +136,59 @@ __device__ __forceinline__ f32x16_t fake_mfma(half4_t a, half4_t b) {   // LVK_M
 #pragma unroll
     for (int i = 0; i < 16; ++i) r[i] = v;
     return r;
+}
+
+// AVX2 horizontal order (ggml.c:2019-2024) and the epilogue of a wave's 32 rows x 16 tokens:
+// lane (h, n, jj) register set c holds chain 2c+jj; r_j = a_j + a_{j+4} (same lane, sets c and
+// c+2), (r0+r2) | (r1+r3) in lanes jj = 0 | 1, then across the lane pair (xor 16)
+template <int EPI>
+__device__ __forceinline__ void mm_store(const MmParams & P, const f32x16_t (&acc)[4], int lane, int w, int m0, int n0) {
+    const int h = lane >> 5;
+    const int jj = (lane >> 4) & 1;
+    float res[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float r0 = acc[0][i] + acc[2][i];       // r_jj     = a_jj + a_{jj+4}
+        const float r2 = acc[1][i] + acc[3][i];       // r_{2+jj} = a_{2+jj} + a_{6+jj}
+        const float v = r0 + r2;
+        res[i] = v + __shfl_xor(v, 16);               // (r0 + r2) + (r1 + r3) in the jj = 0 lanes
+    }
+
+    // ---- epilogue: jj = 0 lanes hold rows 32w + 8q + 4h + p (i = 4q + p) of token n ----
+    const int n = n0 + (lane & 15);
+    if constexpr (EPI == EPI_SWIGLU_F32) {
+        // W1|W3 image interleaved per 4 rows: h = 0 lanes hold the w1 rows, h = 1 the w3 rows of the
+        // same outputs (llama.cpp:1085-1096)
+        float o[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[i] = __shfl_xor(res[i], 32);
+        if (jj == 0 && h == 0 && n < P.N) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float uu[4];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res[4 * q + p])]);  // ggml.c:2495
+                    uu[p] = sl * o[4 * q + p];                                            // llama.cpp:1096
+                }
+                const int row = m0 + 32 * w + 8 * q;
+                *(float4 *) (P.y + (size_t) (P.out_tok0 + n) * P.ldy + row / 2) = make_float4(uu[0], uu[1], uu[2], uu[3]);
+            }
+        }
+    } else {
+        if (jj == 0 && n < P.N) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float4 * yp = (float4 *) (P.y + (size_t) (P.out_tok0 + n) * P.ldy + m0 + 32 * w + 8 * q + 4 * h);
+                if constexpr (EPI == EPI_RESID) {
+                    const float4 r = *yp;                 // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+                    *yp = make_float4(res[4 * q] + r.x, res[4 * q + 1] + r.y, res[4 * q + 2] + r.z, res[4 * q + 3] + r.w);
+                } else {
+                    *yp = make_float4(res[4 * q], res[4 * q + 1], res[4 * q + 2], res[4 * q + 3]);
+                }
+            }
+        }
+    }
 }
 
 // A16: the A fragments come ready-made from the f16 image (one global_load_dwordx2 per
@@ -202,7 +263,10 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
         }
     };
     // A16: lane (rho, h) of wave w reads the fragment of rows m0 + 32w + rho, chain 2c + h
-    const uint4 * a16p = A16 ? (const uint4 *) P.a16 + (size_t) (m0 / 32 + w) * nb * 128 + lane : nullptr;
+    // LVK_MM_EXP & 16 / 32 (probe builds only): every workgroup reads the weights of row tiles 0..3 /
+    // the activations of token tiles 0..1 (always L2-hot; timing only)
+    const int a_rt = (LVK_MM_EXP & 16) ? (rt & 3) : rt;
+    const uint4 * a16p = A16 ? (const uint4 *) P.a16 + (size_t) (a_rt * TM / 32 + w) * nb * 128 + lane : nullptr;
     uint2 aq[A16 ? PDA : 1][4];
     auto load_aq = [&](int blk, uint2 (&q)[4]) {
 #pragma unroll
@@ -214,8 +278,29 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
     };
     // ---- B operand: masked fragments of this token tile, 4 per block ----
     const uint4 * bp = (const uint4 *) P.xm + (size_t) tt * nb * 128 + lane;   // xm_slot pairs
-    constexpr int PB = A16 ? LVK_MM_PDB16 : PD;       // B blocks in flight
+    constexpr bool BL = LVK_MM_BLDS;
+    constexpr int PB = BL ? 1 : A16 ? LVK_MM_PDB16 : PD;       // B blocks in flight
     uint2 bq[PB][4];
+    // BL: sub-chunk u of the token tile is 1024 contiguous uint4; thread tid stages 4 of them
+    const uint4 * bsp = (const uint4 *) P.xm + (size_t) ((LVK_MM_EXP & 32) ? (tt & 1) : tt) * nb * 128 + tid;
+    uint4 bs0, bs1, bs2, bs3;                  // (named: an array of them stays in scratch)
+    auto stage_load = [&](int u) {
+        const uint4 * g = bsp + (size_t) u * 1024;
+        bs0 = g[0]; bs1 = g[NT]; bs2 = g[2 * NT]; bs3 = g[3 * NT];
+    };
+    auto stage_store = [&](int u) {
+        uint4 * bl = (uint4 *) (smem + ((u & 1) ? OFF_B1 : OFF_B0)) + tid;
+        bl[0] = bs0; bl[NT] = bs1; bl[2 * NT] = bs2; bl[3 * NT] = bs3;
+    };
+    auto lds_bq = [&](int u, int jb, uint2 (&q)[4]) {
+        const uint4 * bl = (const uint4 *) (smem + ((u & 1) ? OFF_B1 : OFF_B0)) + jb * 128 + lane;
+#pragma unroll
+        for (int c2 = 0; c2 < 2; ++c2) {
+            const uint4 v = bl[c2 * 64];
+            q[2 * c2] = make_uint2(v.x, v.y);
+            q[2 * c2 + 1] = make_uint2(v.z, v.w);
+        }
+    };
     auto load_bq = [&](int blk, uint2 (&q)[4]) {
 #pragma unroll
         for (int c2 = 0; c2 < 2; ++c2) {
@@ -248,8 +333,13 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
     } else {
         load_a(0, Anext);
     }
+    if constexpr (BL) {
+        stage_load(0);
+        stage_store(0);
+    } else {
 #pragma unroll
-    for (int d = 0; d < PB; ++d) load_bq(min(d, nb - 1), bq[d]);
+        for (int d = 0; d < PB; ++d) load_bq(min(d, nb - 1), bq[d]);
+    }
     store_scales(0);
     if constexpr (!A16) make_x(Anext);
     __syncthreads();
@@ -260,6 +350,7 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
         const bool scales_next = chunk_last && u + 1 < U;
         if (!A16 && u + 1 < U) load_a(u + 1, Anext);
         if (scales_next) load_scales(ch + 1);
+        if (BL && u + 1 < U) stage_load(u + 1);
         const float * wl = (const float *) (smem + ((ch & 1) ? OFF_DW1 : OFF_DW0));
         const float * dl = (const float *) (smem + ((ch & 1) ? OFF_DA1 : OFF_DA0));
         // the block scales s = dw * da (ggml.c:1968) of every (row, token) output come from
@@ -274,6 +365,7 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
             const int blk = 8 * u + jb;
             const uint32_t sel = (jb & 1) ? 0x0C030C02u : 0x0C010C00u;
             uint2 (&bf)[4] = bq[jb % PB];
+            if constexpr (BL) lds_bq(u, jb, bf);
             if ((jb & 1) == 0) {
                 const int jc = (u & 3) * 8 + jb + h;        // block of the chunk this lane half feeds
                 const float dwa = wl[jc * DWS + 32 * w + rho];
@@ -304,67 +396,21 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
                 }
             }
             // refill this slot with block blk + PD (its MFMAs have read the old fragments)
-            load_bq(min(blk + PB, nb - 1), bf);
+            if constexpr (!BL) load_bq(min(blk + PB, nb - 1), bf);
             if constexpr (A16) load_aq(min(blk + PDA, nb - 1), af);
             // block order pinned: unconstrained, hipcc hoists later blocks' MFMAs and spills
 #pragma unroll
             for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(acc[c]));
         }
         if (!A16 && u + 1 < U) make_x(Anext);
-        if (scales_next) {
-            store_scales(ch + 1);
-            __syncthreads();            // chunk ch+1's scales visible; chunk ch-1's buffer free again
-        }
+        if (BL && u + 1 < U) stage_store(u + 1);
+        if (scales_next) store_scales(ch + 1);
+        if (scales_next || (BL && u + 1 < U))
+            __syncthreads();            // chunk ch+1's scales / sub-chunk u+1's B visible; the buffers of
+                                        // chunk ch-1 / sub-chunk u-1 free again
     }
 
-    // ---- AVX2 horizontal order (ggml.c:2019-2024): lane (h, n, jj) register set c holds chain 2c+jj;
-    // r_j = a_j + a_{j+4} (same lane, sets c and c+2), (r0+r2) | (r1+r3) in lanes jj = 0 | 1, then across
-    // the lane pair (xor 16)
-    const int jj = (lane >> 4) & 1;
-    float res[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const float r0 = acc[0][i] + acc[2][i];       // r_jj     = a_jj + a_{jj+4}
-        const float r2 = acc[1][i] + acc[3][i];       // r_{2+jj} = a_{2+jj} + a_{6+jj}
-        const float v = r0 + r2;
-        res[i] = v + __shfl_xor(v, 16);               // (r0 + r2) + (r1 + r3) in the jj = 0 lanes
-    }
-
-    // ---- epilogue: jj = 0 lanes hold rows 32w + 8q + 4h + p (i = 4q + p) of token n ----
-    const int n = n0 + (lane & 15);
-    if constexpr (EPI == EPI_SWIGLU_F32) {
-        // W1|W3 image interleaved per 4 rows: h = 0 lanes hold the w1 rows, h = 1 the w3 rows of the
-        // same outputs (llama.cpp:1085-1096)
-        float o[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[i] = __shfl_xor(res[i], 32);
-        if (jj == 0 && h == 0 && n < P.N) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float uu[4];
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res[4 * q + p])]);  // ggml.c:2495
-                    uu[p] = sl * o[4 * q + p];                                            // llama.cpp:1096
-                }
-                const int row = m0 + 32 * w + 8 * q;
-                *(float4 *) (P.y + (size_t) (P.out_tok0 + n) * P.ldy + row / 2) = make_float4(uu[0], uu[1], uu[2], uu[3]);
-            }
-        }
-    } else {
-        if (jj == 0 && n < P.N) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float4 * yp = (float4 *) (P.y + (size_t) (P.out_tok0 + n) * P.ldy + m0 + 32 * w + 8 * q + 4 * h);
-                if constexpr (EPI == EPI_RESID) {
-                    const float4 r = *yp;                 // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
-                    *yp = make_float4(res[4 * q] + r.x, res[4 * q + 1] + r.y, res[4 * q + 2] + r.z, res[4 * q + 3] + r.w);
-                } else {
-                    *yp = make_float4(res[4 * q], res[4 * q + 1], res[4 * q + 2], res[4 * q + 3]);
-                }
-            }
-        }
-    }
+    mm_store<EPI>(P, acc, lane, w, m0, n0);
 }
 
 // ---------------------------------------------------------------------------
@@ -565,8 +611,8 @@ hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, 
     const dim3 grid((w.M / TM) * P.ntt);
 #define LVK_MM_GO(E)                                                                      \
     do {                                                                                  \
-        if (P.a16) LVK_LAUNCH((k_mm_q40_mfma<E, true>), grid, dim3(NT), LDS_TOTAL, s, P); \
-        else LVK_LAUNCH((k_mm_q40_mfma<E, false>), grid, dim3(NT), LDS_TOTAL, s, P);      \
+        if (P.a16) LVK_LAUNCH((k_mm_q40_mfma<E, true>), grid, dim3(NT), LVK_MM_BLDS ? LDS_TOTAL_BL : LDS_TOTAL, s, P); \
+        else LVK_LAUNCH((k_mm_q40_mfma<E, false>), grid, dim3(NT), LVK_MM_BLDS ? LDS_TOTAL_BL : LDS_TOTAL, s, P); \
     } while (0)
     switch (epi) {
         case EPI_STORE: LVK_MM_GO(EPI_STORE); break;

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 #include "lvk_kernels.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1);} } while (0)
 using namespace lvk;
@@ -48,7 +49,19 @@ int main(int argc, char ** argv) {
             q.a16 = a16;
         }
         CK(launch_act_f16(x, nullptr, N, s.K, xh, da, 0));
-        for (int i = 0; i < 2; ++i) CK(launch_mm_mfma(q, xh, da, N, y, s.M, 0, s.epi, stab, 0));
+        const int ldy = s.epi == EPI_SWIGLU_F32 ? s.M / 2 : s.M;
+        // one launch on a zeroed y: FNV hash of the output bits (variants must agree)
+        CK(hipMemset(y, 0, (size_t) N * ldy * 4));
+        CK(launch_mm_mfma(q, xh, da, N, y, ldy, 0, s.epi, stab, 0));
+        CK(hipDeviceSynchronize());
+        {
+            std::vector<uint32_t> h((size_t) N * ldy);
+            CK(hipMemcpy(h.data(), y, h.size() * 4, hipMemcpyDeviceToHost));
+            uint64_t f = 1469598103934665603ull;
+            for (uint32_t v : h) { f ^= v; f *= 1099511628211ull; }
+            printf("%-4s hash %016llx\n", s.name, (unsigned long long) f);
+        }
+        for (int i = 0; i < 2; ++i) CK(launch_mm_mfma(q, xh, da, N, y, ldy, 0, s.epi, stab, 0));
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(e0, 0));
         for (int i = 0; i < reps; ++i) CK(launch_mm_mfma(q, xh, da, N, y, s.epi == EPI_SWIGLU_F32 ? s.M / 2 : s.M, 0, s.epi, stab, 0));
