@@ -169,8 +169,6 @@ struct AttnDArgs {
     unsigned * err;               // host-mapped error word (nullptr: none)
     int short_max;                // n_kv <= short_max: no score exchange (every workgroup scores all)
     int seq_epochs;               // epoch += sp->seq << 7 (granules never zeroed between tokens)
-    int vorder;                   // V chunk-0 DMA (LVK_ATTN_VORDER, A/B): 0 before the n_past-dependent
-                                  // K loads, 1 after them, 2 with the rest of V behind the first scores
 };
 
 // The 4 workgroups of a head either split the scores and exchange them as granules, or
@@ -198,10 +196,10 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     // this layer's granule tag: unique per (step, layer) when the step counter is used
     const unsigned ep = A.seq_epochs ? A.epoch + (spc->seq << 7) : A.epoch;
 
-    // 1a. Loads that do not depend on n_past go out before the step block is read: Q,
-    // the K rows of positions 0..63 (chunk 0; rows past n_kv are read, never used) and the
-    // V slice of positions 0..63.  A short context (n_kv <= 64, no exchange) then has all
-    // its operands in flight from the first cycle.
+    // 1a. Loads that do not depend on n_past go out before the step block is read: Q and
+    // the K rows of positions 0..63 (chunk 0; rows past n_kv are read, never used).  A short
+    // context (n_kv <= 64, no exchange) then has its score operands in flight from the
+    // first cycle; V follows behind the first scores (1b).
     const uint4 * qp = (const uint4 *) (A.q16 + h * HD) + r;
     uint4 qv[4];
 #pragma unroll
@@ -223,7 +221,6 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
 #pragma unroll
         for (int st = 0; st < 4; ++st) kv[0][st] = kp[st * 4];
     }
-    if (A.vorder == 0) v_dma(0, 0, 64);
     const int n_kv = n_past + 1;
     const int n_pad = (n_kv + 31) & ~31;
     const int np = n_kv & ~31;
@@ -245,7 +242,6 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
 #pragma unroll
         for (int st = 0; st < 4; ++st) kv[1][st] = kp[st * 4];
     }
-    if (A.vorder == 1) v_dma(0, 0, 64);
     LVK_DT(6);
 
     // 1b. scores of chunks sl, sl+4, ... (exchange) or of every chunk (one position per lane quad)
@@ -278,9 +274,11 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
         if (c0_other) score(kx, cb + (tid >> 2));
         else score(kv[0], cb + (tid >> 2));          // cb < n_kv: sl * 64 < n_kv when c0_other
         if (cb + cs < n_kv) score(kv[1], cb + cs + (tid >> 2));
-        // the rest of the V slice goes out behind the first two chunks' scores: those wait
-        // only for their own K rows, the V rows are needed after the softmax
-        for (int p0 = 0; p0 < n_pad; p0 += 512) v_dma(p0, A.vorder == 2 ? 0 : 64, n_pad);
+        // the V slice goes out behind the first two chunks' scores: those wait only for their
+        // own K rows, the V rows are needed after the softmax.  (Chunk 0 of V issued with Q
+        // and K chunk 0, or right after the n_past-dependent K loads: 5.66-5.73 / 5.71-5.77 us
+        // against 5.42-5.47 us per launch here, 7B decode_speed, profiles/r04_attn_vorder.jsonl)
+        for (int p0 = 0; p0 < n_pad; p0 += 512) v_dma(p0, 0, n_pad);
         LVK_DT(7);
         LVK_DT(1);
         for (int c0 = cb + 2 * cs; c0 < n_kv; c0 += cs) {
@@ -712,8 +710,6 @@ AttnDArgs attn_args(const AttnLaunch & A, void * gran, unsigned epoch) {
     }();
     a.short_max = short_max;
     a.seq_epochs = A.seq_epochs;
-    static const int vorder = [] { const char * e = getenv("LVK_ATTN_VORDER"); return e ? atoi(e) : 0; }();
-    a.vorder = vorder;
     return a;
 }
 
