@@ -109,6 +109,12 @@ LVK_API void lvk_set_graph(struct llama_context * ctx, int on);
 LVK_API void lvk_set_decode_persistent(struct llama_context * ctx, int on);
 /* 1 when the next single-token eval of ctx runs the persistent kernel */
 LVK_API int lvk_decode_persistent_active(struct llama_context * ctx);
+/* how ctx's single-token evals run each layer's decode attention: 0 = its own launch after
+ * QKV (default), 1 = beside the QKV launch on a second stream (env LVK_ATTN_BESIDE=1), 2 =
+ * inside the QKV launch (env LVK_QKV_ATTN=1, 7B shapes).  1 and 2 hand the new q / k / v rows
+ * over as tagged granules; each is chosen at context creation only where the workgroups of
+ * both roles are guaranteed co-resident (else 0) */
+LVK_API int lvk_attn_mode(struct llama_context * ctx);
 
 /* On-device greedy sampling.  lvk_eval_greedy(ctx, token, n_past)
  * is llama_eval(ctx, &token, 1, n_past, .) followed by

@@ -28,9 +28,22 @@ struct EventSplit {
     ~EventSplit() { g_launch_events = saved; }
 };
 
+// resource footprint of the kernel a launcher would start (g_footprint set: LVK_LAUNCH records
+// it instead of launching; used to check that two launches can be resident together)
+struct KernelFootprint {
+    int threads = 0;            // per workgroup
+    int vgprs = 0;              // per lane (architected + accumulation registers)
+    size_t lds = 0;             // per workgroup, static + dynamic
+    int workgroups = 0;
+};
+extern thread_local KernelFootprint * g_footprint;
+void record_footprint(const void * fn, dim3 grid, dim3 block, size_t lds);
+
 #define LVK_LAUNCH(kern, grid, block, lds, stream, ...)                                                        \
     do {                                                                                                       \
-        if (::lvk::g_launch_events.start || ::lvk::g_launch_events.stop)                                       \
+        if (::lvk::g_footprint)                                                                                \
+            ::lvk::record_footprint(reinterpret_cast<const void *>(kern), grid, block, lds);                   \
+        else if (::lvk::g_launch_events.start || ::lvk::g_launch_events.stop)                                  \
             hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ::lvk::g_launch_events.start,                \
                                   ::lvk::g_launch_events.stop, 0, __VA_ARGS__);                                \
         else                                                                                                   \
@@ -114,6 +127,8 @@ struct MvLaunch {
     RopeTable rope{};
     int n_embd = 0, head_dim = 0, n_ctx = 0;
     int kv32 = 0;                    // f32 KV cache and f32 queries (f16_kv = false)
+    unsigned long long * qkv_gran = nullptr;   // decode (matvec_cu*): also publish the q / k / v rows
+    unsigned qkv_epoch = 0;                    // as granules tagged qkv_epoch + (seq << 7) (see AttnLaunch)
     // EPI_SWIGLU
     const uint16_t * silu_tab = nullptr;   // 64Ki fp16 table
     ActQ out_q;                            // quantized u = silu(w1 x) * (w3 x)
@@ -155,6 +170,11 @@ struct AttnLaunch {
     unsigned * err = nullptr; // host-mapped error word (DevError); kernels that spin report a timeout here
     int kv32 = 0;             // f32 K, V and queries (f16_kv = false): launch_attention only
     int seq_epochs = 0;       // decode attention: granule epoch = (sp->seq << 7) + epoch (no per-token zeroing)
+    // decode attention beside QKV: the new position's q / k / v come from these granules
+    // ([3][E/2], written by the QKV launch running at the same time, MvLaunch::qkv_gran),
+    // not from q16 / kc / vc; needs seq_epochs
+    const unsigned long long * qkv_gran = nullptr;
+    size_t lds_min = 0;       // decode attention: request at least this much LDS (caps workgroups per CU)
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
 // prompt batches (N > 1, Q4_0 / Q4_1 output): scores+softmax per (head, 32 tokens) then
@@ -175,6 +195,15 @@ hipError_t exp_check(const uint16_t * exp_tab, int * bad_d, hipStream_t s);
 bool attention_decode_supported(int n_embd, int n_head, int n_ctx);
 size_t attention_decode_scratch_bytes(int n_head, int n_ctx);
 hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned epoch, hipStream_t s);
+// QKV (the CU-balanced matvec with the RoPE / KV epilogue, L.qkv_gran set) and the decode
+// attention of the same layer in one launch (matvec_cu.hip k_qkv_attn; 7B shapes, Q4_0):
+// cnt / cons are [H] counters QKV_CNT_STRIDE words apart (one 128-B line each: the
+// agent-scope atomics of different heads must not share a line), zero at the first launch
+// and left zero by each launch
+constexpr int QKV_CNT_STRIDE = 32;
+bool qkv_attn_supported(const QMatrix & w, int n_embd, int n_head, int n_ctx);
+hipError_t launch_qkv_attn(const MvLaunch & L, const AttnLaunch & A, void * gran, unsigned epoch, unsigned * cnt,
+                           unsigned * cons, hipStream_t s);
 // the same attention + the Wo matvec + residual add (y += Wo attn) in ONE launch
 // (attention_decode.hip, k_attn_wo): Q4_0 Wo with K = 4096 and every workgroup
 // resident (n_ctx <= 1024 here); the attention output reaches the Wo workgroups

@@ -44,6 +44,8 @@ struct Cu41Params {
     int n_embd, head_dim, n_ctx;
     int kv32;                   // f32 KV cache and queries (f16_kv = false)
     const uint16_t * silu_tab;
+    unsigned long long * qkv_gran;   // EPI_QKV: also publish q / k / v granules (nullptr: no)
+    unsigned qkv_epoch;             // their tag base (layer + 1; + seq << 7)
 };
 
 // per-wave block-product tables in LDS: 4 tables (s, dx*my, mx*dy, mx*my) of 8 rows x 32
@@ -289,25 +291,10 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
         } else if constexpr (EPI == EPI_RESID) {
             if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
         } else if constexpr (EPI == EPI_QKV) {
-            const int E = P.n_embd, hd = P.head_dim;
-            const int which = row / E;          // 0 q, 1 k, 2 v (uniform per wave: E % 8 == 0)
-            const int e = row - which * E;
-            const int pos = P.sp->n_past;
-            const float other_r = __shfl_xor(res, 8);   // row e^1 lives in lanes of row r^1
-            if (j == 0) {
-                if (which < 2) {
-                    // ggml_compute_forward_rope_f32 mode 0 (ggml.c:7209-7223)
-                    const int i0 = e % hd;
-                    const float2 cs = P.rope[(size_t) pos * (hd / 2) + (i0 >> 1)];
-                    float out;
-                    if ((i0 & 1) == 0) { const float a = res * cs.x, b = other_r * cs.y; out = a - b; }
-                    else               { const float a = other_r * cs.y, b = res * cs.x; out = a + b; }
-                    if (which == 0) kv_store(P.q16, e, out, P.kv32);
-                    else            kv_store(P.kc, (size_t) pos * E + e, out, P.kv32);
-                } else {
-                    kv_store(P.vc, (size_t) e * P.n_ctx + pos, res, P.kv32);
-                }
-            }
+            const StepParams * sp = P.sp;
+            const unsigned ep = P.qkv_gran ? P.qkv_epoch + (sp->seq << 7) : 0u;
+            qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32,
+                         P.qkv_gran, ep);
         } else if constexpr (EPI == EPI_SWIGLU_F32) {
             // fused W1|W3 image interleaved per 4 rows: rows 0-3 of the group are
             // w1 rows 4grp..4grp+3, rows 4-7 the w3 rows (llama.cpp:1085-1096)
@@ -370,6 +357,8 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
     P.q16 = L.q16; P.kc = L.kc; P.vc = L.vc; P.rope = L.rope.cs;
     P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx; P.kv32 = L.kv32;
     P.silu_tab = L.silu_tab;
+    P.qkv_gran = L.qkv_gran;
+    P.qkv_epoch = L.qkv_epoch;
     const int K = L.w.K;
 #ifdef LVK_PROBE_SWEEP   // dev probe builds only: LVK_CFG41 selects a launch shape (waves, prefetch depth)
     {

@@ -76,6 +76,9 @@ Context::~Context() {
     if (sp_h) (void) hipHostFree(sp_h);
     if (tok_h) (void) hipHostFree(tok_h);
     if (err_h) (void) hipHostFree(err_h);
+    if (ev_fork) (void) hipEventDestroy(ev_fork);
+    if (ev_join) (void) hipEventDestroy(ev_join);
+    if (side) (void) hipStreamDestroy(side);
     if (stream) (void) hipStreamDestroy(stream);
 }
 
@@ -125,6 +128,29 @@ void Context::init(const llama_context_params & p) {
         LVK_HIP(hipMemset(attn_gran, 0, attention_decode_scratch_bytes((int) H, (int) C)));
         // granule tags (seq << 7) + layer + 1 stay unique per token with up to 126 layers
         seq_epochs = !fuse_attn_wo && L <= 126;
+        // the decode attention beside QKV: every QKV workgroup and the 4 H attention workgroups
+        // are resident together (one QKV workgroup per CU, the attention's LDS beside it), the
+        // granule waits are bounded (error word) -- LVK_ATTN_BESIDE=1
+        attn_beside = seq_epochs && !kv32 && attention_decode_supported((int) E, (int) H, (int) C) &&
+                      matvec_cu_supported((int) E, model.qtype) && getenv("LVK_ATTN_BESIDE") &&
+                      atoi(getenv("LVK_ATTN_BESIDE")) != 0 && beside_fits();
+        qkv_attn = seq_epochs && !kv32 && !attn_beside && model.qtype == Q4_0 && !model.layers.empty() &&
+                   qkv_attn_supported(model.layers[0].wqkv, (int) E, (int) H, (int) C) && getenv("LVK_QKV_ATTN") &&
+                   atoi(getenv("LVK_QKV_ATTN")) != 0;
+        if (attn_beside || qkv_attn) {
+            qkv_gran = (unsigned long long *) model.alloc(3 * (E / 2) * 8);
+            LVK_HIP(hipMemset(qkv_gran, 0, 3 * (E / 2) * 8));
+        }
+        if (qkv_attn) {
+            qkv_cnt = (unsigned *) model.alloc(2 * H * QKV_CNT_STRIDE * 4);
+            qkv_cons = qkv_cnt + H * QKV_CNT_STRIDE;
+            LVK_HIP(hipMemset(qkv_cnt, 0, 2 * H * QKV_CNT_STRIDE * 4));
+        }
+        if (attn_beside) {
+            LVK_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+            LVK_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+            LVK_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+        }
         // test hook (tests/test_gpu_seq_wrap.py): start the step counter near its 25-bit wrap
         if (const char * e = getenv("LVK_SEQ_START")) seq = (unsigned) strtoul(e, nullptr, 0) & ((1u << 25) - 1);
     }
@@ -392,6 +418,10 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
     const bool attn_wo = n == 1 && !old_attention && !kv32 && fuse_attn_wo && model.qtype == Q4_0 && !model.layers.empty() &&
                          attention_wo_supported(E, H, n_ctx, model.layers[0].wo);
     const bool seq_ep = seq_epochs && !attn_wo;
+    // (the QKV launch must be the CU-balanced kernel: only its epilogue publishes the granules)
+    const bool beside = attn_beside && n == 1 && !old_attention && !kv32 && seq_ep &&
+                        attention_decode_supported(E, H, n_ctx) && matvec_cu_supported(E, model.qtype);
+    const bool merged = qkv_attn && n == 1 && !old_attention && !kv32 && seq_ep;
     if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx) && !seq_ep)
         // the decode attention's score granules carry epoch = layer + 1: zero them once per token
         LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes(H, n_ctx), stream));
@@ -406,18 +436,44 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
         a.w = ly.wqkv; a.x = x; a.g = ly.attn_norm; a.sp = sp_d; a.n_tokens = n;
         a.q16 = q16; a.kc = kc_layer(il); a.vc = vc_layer(il); a.rope.cs = rope;
         a.n_embd = E; a.head_dim = hd; a.n_ctx = n_ctx; a.kv32 = kv32;
-        timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
         AttnLaunch at{q16, kc_layer(il), vc_layer(il), scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
         at.exp_computed = exp_computed;
         at.err = err_d;
         at.kv32 = kv32;
         at.seq_epochs = seq_ep ? 1 : 0;
+        const bool beside_l = beside && !attn_wo;
+        const bool merged_l = merged && !attn_wo;
+        if (merged_l) {
+            a.qkv_gran = qkv_gran;
+            a.qkv_epoch = (unsigned) il + 1;
+        }
+        if (beside_l) {
+            // fork: the attention of this layer on the side stream, from the same point as QKV
+            // (after W2 of the previous layer), joined again before Wo
+            a.qkv_gran = qkv_gran;
+            a.qkv_epoch = (unsigned) il + 1;
+            at.qkv_gran = qkv_gran;
+            at.lds_min = attn_lds_min;
+            LVK_HIP(hipEventRecord(ev_fork, stream));
+            LVK_HIP(hipStreamWaitEvent(side, ev_fork, 0));
+            timed_launch(K_ATTN, 0, [&] { return launch_attention_decode(at, attn_gran, (unsigned) il + 1, side); });
+            LVK_HIP(hipEventRecord(ev_join, side));
+        }
+        if (merged_l)
+            timed_launch(K_QKV, qbytes(ly.wqkv), [&] {
+                return launch_qkv_attn(a, at, attn_gran, (unsigned) il + 1, qkv_cnt, qkv_cons, stream);
+            });
+        else
+            timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
+        if (beside_l) LVK_HIP(hipStreamWaitEvent(stream, ev_join, 0));
         if (attn_wo) {
             timed_launch(K_ATTN_WO, qbytes(ly.wo), [&] {
                 return launch_attention_wo(at, ly.wo, x, attn_gran, (unsigned) il + 1, stream);
             });
         } else {
-            if (n > 1 && !kv32 && attention_prompt_supported(E, H, n_ctx))
+            if (beside_l || merged_l)
+                ;   // launched on the side stream / inside the QKV launch above
+            else if (n > 1 && !kv32 && attention_prompt_supported(E, H, n_ctx))
                 timed_launch(K_ATTN, 0, [&] {
                     return launch_attention_prompt(at, (uint16_t *) scores, nullptr, nullptr, stream);
                 });
@@ -508,6 +564,46 @@ int Context::eval_greedy(int token, int n_past) {
     return *greedy_h;
 }
 
+int Context::attn_mode() const { return qkv_attn ? 2 : attn_beside ? 1 : 0; }
+
+// the decode attention beside QKV is safe only if, wherever the dispatcher puts the 4 H
+// attention workgroups, every QKV workgroup can still be placed: the attention requests
+// more than half a CU's LDS (at most one per CU), 4 H <= CUs, and one attention workgroup
+// plus one QKV workgroup fit a CU's LDS, wave slots and each SIMD's 512 registers (footprints
+// of the exact kernels, LVK_LAUNCH's record mode).  Otherwise the attention stays after QKV.
+bool Context::beside_fits() {
+    const HParams & hp = model.hp;
+    const int E = (int) hp.n_embd, H = (int) hp.n_head;
+    KernelFootprint fq, fa;
+    {
+        MvLaunch a;
+        a.w.qtype = model.qtype; a.w.M = 3 * E; a.w.K = E;
+        a.n_tokens = 1; a.n_embd = E; a.head_dim = E / H; a.n_ctx = n_ctx;
+        g_footprint = &fq;
+        const hipError_t e = launch_matvec_cu(a, PRO_NORM, EPI_QKV, nullptr);
+        g_footprint = nullptr;
+        if (e != hipSuccess || !fq.threads) return false;
+    }
+    {
+        static const unsigned long long dummy = 0;
+        AttnLaunch at{};
+        at.out_qtype = model.qtype; at.n_tokens = 1; at.n_embd = E; at.n_head = H; at.n_ctx = n_ctx;
+        at.seq_epochs = 1; at.qkv_gran = &dummy;
+        g_footprint = &fa;
+        const hipError_t e = launch_attention_decode(at, nullptr, 1, nullptr);
+        g_footprint = nullptr;
+        if (e != hipSuccess || !fa.threads) return false;
+    }
+    constexpr size_t LDS_CU = 160 * 1024;
+    const size_t pad = std::max(fa.lds, LDS_CU / 2 + 1024);
+    auto alloc = [](int v) { return (std::max(v, 1) + 7) / 8 * 8; };
+    const int wq = fq.threads / 64, wa = fa.threads / 64;
+    const bool ok = fa.workgroups <= cu_count() && fq.lds + pad <= LDS_CU && wq + wa <= 32 &&
+                    alloc(fq.vgprs) * ((wq + 3) / 4) + alloc(fa.vgprs) * ((wa + 3) / 4) <= 512;
+    if (ok) attn_lds_min = pad;
+    return ok;
+}
+
 // the step counter of the next device step (StepParams::seq); before it would run past the
 // 25 bits that keep (seq << 7) + layer + 1 unique, the granules are zeroed (stream-ordered
 // ahead of the steps that use the restarted counter) and the count restarts
@@ -515,6 +611,7 @@ unsigned Context::next_seq(unsigned k) {
     if (seq + k >= (1u << 25)) {
         if (attn_gran)
             LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes((int) model.hp.n_head, n_ctx), stream));
+        if (qkv_gran) LVK_HIP(hipMemsetAsync(qkv_gran, 0, 3 * (model.hp.n_embd / 2) * 8, stream));
         seq = 0;
     }
     const unsigned first = seq + 1;

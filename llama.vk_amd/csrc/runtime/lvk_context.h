@@ -103,6 +103,20 @@ struct Context {
     // measured slower than the two launches (17.7 vs 11.5 us per layer at n_past 256), so off
     bool fuse_attn_wo = false;
     void * attn_gran = nullptr;  // [H][n_ctx] {tag, score} granules of the decode attention  // env LVK_ATTN_V1=1: single-token evals on the one-kernel attention.hip
+    // decode attention beside QKV (LVK_ATTN_BESIDE): the attention of layer l runs on a second
+    // stream next to QKV(l) and takes the new q / k / v rows as tagged granules
+    bool attn_beside = false;
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    unsigned long long * qkv_gran = nullptr;   // [3][E/2] {tag, f16 pair}
+    size_t attn_lds_min = 0;                   // the attention's LDS request beside QKV
+    bool beside_fits();
+    // QKV and the decode attention in one launch (LVK_QKV_ATTN; matvec_cu.hip k_qkv_attn)
+    bool qkv_attn = false;
+    unsigned * qkv_cnt = nullptr;              // [H] QKV row groups finished per head
+    unsigned * qkv_cons = nullptr;             // [H] attention workgroups that have read them
+    // 0: the decode attention after QKV, 1: beside it on a second stream, 2: merged into it
+    int attn_mode() const;
     uint16_t * xh = nullptr;     // masked MFMA B-fragment image of the quantized activations (mm_act_bytes)
     float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales
     void * xside = nullptr;      // Q4_1: the activations' side image (mm41_act_side_bytes)

@@ -1,5 +1,6 @@
 // lvk_ops.cpp -- operator-level C ABI (include/lvk_ops.h): each op runs the
 // production kernel on host buffers so tests can pin it against the oracle.
+#include <algorithm>
 #include <immintrin.h>
 
 #include <cstdio>
@@ -320,6 +321,11 @@ void lvk_set_graph(struct llama_context * ctx, int on) {
 }
 void lvk_set_decode_persistent(struct llama_context * ctx, int on) {
     for (lvk::Context * c : ctx->stages()) c->set_decode_persistent(on != 0);
+}
+int lvk_attn_mode(struct llama_context * ctx) {
+    int m = -1;
+    for (lvk::Context * c : ctx->stages()) m = m < 0 ? c->attn_mode() : std::min(m, c->attn_mode());
+    return m < 0 ? 0 : m;
 }
 int lvk_decode_persistent_active(struct llama_context * ctx) {
     for (lvk::Context * c : ctx->stages())

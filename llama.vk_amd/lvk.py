@@ -111,6 +111,7 @@ _sig("lvk_set_graph", None, [C.c_void_p, C.c_int])
 _sig("lvk_set_decode_persistent", None, [C.c_void_p, C.c_int])
 _sig("lvk_decode_persistent_active", C.c_int, [C.c_void_p])
 _sig("lvk_set_prompt_exact", None, [C.c_void_p, C.c_int])
+_sig("lvk_attn_mode", C.c_int, [C.c_void_p])
 _sig("lvk_eval_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_decode_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p])
 _sig("lvk_argmax", C.c_int, [f32p, C.c_int])
@@ -300,6 +301,10 @@ class Llama:
 
     def decode_persistent_active(self):
         return bool(lib.lvk_decode_persistent_active(self.ctx))
+
+    def attn_mode(self):
+        """decode attention: 0 after QKV, 1 beside it on a second stream, 2 inside the QKV launch"""
+        return int(lib.lvk_attn_mode(self.ctx))
 
     def set_prompt_exact(self, on):
         """prompt batches on the bit-faithful VALU path (True) or the MFMA path (False, default)"""

@@ -109,7 +109,7 @@ def test_eval_errors(lvk, tiny_models):
 def test_7b_shaped_decode_vs_oracle(lvk, oracle, model_dir, n_prompt):
     """LLaMA-7B layer shapes (n_embd 4096, n_ff 11008, 32 heads) with 2 layers:
     the decode path runs the CU-balanced kernels compiled for K = 4096 / 11008
-    (matvec_cu.hip, matvec_dma.hip); the 8-token prompt runs the generic kernels, the
+    (matvec_cu.hip); the 8-token prompt runs the generic kernels, the
     24-token one the MFMA matmuls.  Bit-exact vs oracle."""
     from oracle_lib import gen_model, prompt_tokens
     path = gen_model(os.path.join(model_dir, "w4096_l2.bin"), n_embd=4096, n_head=32, n_layer=2, ftype=2, seed=7)
