@@ -23,6 +23,8 @@
 #include "lvk_kernels.h"
 #include "matvec_common.h"
 
+#include <cstdlib>
+
 namespace lvk {
 
 namespace {
@@ -56,7 +58,12 @@ __device__ __forceinline__ float quad_reduce(const float s[8]) {
 // ---------------------------------------------------------------------------
 // scores + softmax.  T query tokens per workgroup, 256 threads = 64 quads.
 // ---------------------------------------------------------------------------
-template <int T>
+// SV 1: a lane per position and a wave per token (4 waves: tokens w, w+4, ...): the lane keeps
+// its K row packed (64 VGPRs) and runs all 32 AVX accumulators of ggml_vec_dot_f16 itself
+// with v_fma_mix (f16 operands converted exactly, one rounding), then the F32Cx8 reduce in
+// registers -- 159 instructions per score instead of 4 lanes x ~125 (a quad per position:
+// cross-lane reduce, per-token Q conversion)
+template <int T, int SV>
 __global__ __launch_bounds__(256) void k_attn_p_scores(const uint16_t * __restrict__ q16, const uint16_t * __restrict__ kc,
                                                        const uint16_t * __restrict__ exp_tab, const StepParams * sp,
                                                        int E, int n_ctx, float scale, uint16_t * __restrict__ P,
@@ -77,7 +84,50 @@ __global__ __launch_bounds__(256) void k_attn_p_scores(const uint16_t * __restri
     }
     __syncthreads();
 
-    // ---- scores: quad `quad` owns position p = pb + quad of each 64-position tile ----
+    if constexpr (SV == 1) {
+        // ---- scores: lane owns position p = pb + lane of each 64-position tile, wave w tokens w, w+4, ..
+        for (int pb = 0; pb <= lim_hi; pb += 64) {
+            const int p = pb + lane;
+            const bool live = p <= lim_hi;
+            uint4 kr[16];
+            const uint4 * kp = (const uint4 *) (kc + (size_t) min(p, lim_hi) * E + h * HD);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) kr[i] = kp[i];
+            for (int t = wave; t < nt; t += 4) {
+                // accumulator (j, l) of ggml_vec_dot_f16 (ggml.c:1781-1815): elements 32 st + 8 j + l,
+                // st = 0..3 in order; uint4 4 st + j holds the 8 of (st, j), word w elements 2w, 2w + 1
+                float acc[4][8];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int l = 0; l < 8; ++l) acc[j][l] = 0.0f;
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint4 q = qs[t * 16 + 4 * st + j];          // wave-uniform: an LDS broadcast
+                        const uint4 k = kr[4 * st + j];
+                        const uint32_t qw[4] = {q.x, q.y, q.z, q.w}, kw[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+                        for (int w = 0; w < 4; ++w) {
+                            acc[j][2 * w] = fma_mix_hh<0, 0>(kw[w], qw[w], acc[j][2 * w]);
+                            acc[j][2 * w + 1] = fma_mix_hh<1, 1>(kw[w], qw[w], acc[j][2 * w + 1]);
+                        }
+                    }
+                }
+                // F32Cx8 reduce in the order of quad_reduce (accumulator j = quad lane j there)
+                float S[8];
+#pragma unroll
+                for (int l = 0; l < 8; ++l) {
+                    const float a = acc[0][l] + acc[1][l], b = acc[2][l] + acc[3][l];
+                    S[l] = a + b;
+                }
+                const float t0v = S[0] + S[4], t1v = S[1] + S[5], t2v = S[2] + S[6], t3v = S[3] + S[7];
+                const float kq = (t0v + t1v) + (t2v + t3v);
+                if (live) sc[(size_t) t * n_ctx + p] = p <= n_past + t0 + t ? kq * scale : -INFINITY;
+            }
+        }
+    } else
     for (int pb = 0; pb <= lim_hi; pb += 64) {
         const int p = pb + quad;
         const bool live = p <= lim_hi;
@@ -286,8 +336,13 @@ hipError_t launch_attention_prompt(const AttnLaunch & A, uint16_t * p_scratch, v
     EventSplit ev;
     ev.first();
     const size_t lds1 = (size_t) T * 256 + (size_t) T * A.n_ctx * 4;
-    LVK_LAUNCH(k_attn_p_scores<T>, dim3(A.n_head, (A.n_tokens + T - 1) / T), dim3(256), lds1, s, A.q16, A.kc,
-               A.exp_tab, A.sp, A.n_embd, A.n_ctx, scale, p_scratch, A.exp_computed);
+    static const int sv = [] { const char * e = getenv("LVK_ATTN_P_SV"); return e ? atoi(e) : 1; }();
+    if (sv == 1)
+        LVK_LAUNCH((k_attn_p_scores<T, 1>), dim3(A.n_head, (A.n_tokens + T - 1) / T), dim3(256), lds1, s, A.q16, A.kc,
+                   A.exp_tab, A.sp, A.n_embd, A.n_ctx, scale, p_scratch, A.exp_computed);
+    else
+        LVK_LAUNCH((k_attn_p_scores<T, 0>), dim3(A.n_head, (A.n_tokens + T - 1) / T), dim3(256), lds1, s, A.q16, A.kc,
+                   A.exp_tab, A.sp, A.n_embd, A.n_ctx, scale, p_scratch, A.exp_computed);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds2 = (size_t) 64 * A.n_ctx * 2;

@@ -159,4 +159,18 @@ __device__ __forceinline__ void mm_tile(int L, int ntt, int nrt, int supertile, 
     }
 }
 
+// fmaf(f16 half HA of a, f16 half HB of b, c): v_fma_mix converts both f16 operands
+// exactly and rounds once, the same result as fmaf on the converted values
+template <int HA, int HB>
+__device__ __forceinline__ float fma_mix_hh(uint32_t a, uint32_t b, float c) {
+    float d;
+    if constexpr (HA == 0 && HB == 0)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[1,1,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    else if constexpr (HA == 1 && HB == 1)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    else
+        static_assert(HA == HB, "same halves only");
+    return d;
+}
+
 }  // namespace lvk
