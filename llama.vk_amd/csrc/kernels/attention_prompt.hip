@@ -54,6 +54,20 @@ __device__ __forceinline__ float quad_reduce(const float s[8]) {
     return (t0 + t1) + (t2 + t3);
 }
 
+// the same sums by two DPP butterflies: (v0 + v1) + (v2 + v3) in every lane of the quad (fp
+// addition is commutative, so lane 1's v1 + v0 and lane 2's (v2 + v3) + (v0 + v1) are the same
+// bits) -- 4 instructions per accumulator instead of 7
+__device__ __forceinline__ float quad_reduce_bf(const float s[8]) {
+    float S[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        const float x = s[l];
+        const float y = x + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+        S[l] = y + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, y), 0x4E, 0xF, 0xF, false));
+    }
+    const float t0 = S[0] + S[4], t1 = S[1] + S[5], t2 = S[2] + S[6], t3 = S[3] + S[7];
+    return (t0 + t1) + (t2 + t3);
+}
 
 // ---------------------------------------------------------------------------
 // scores + softmax.  T query tokens per workgroup, 256 threads = 64 quads.
@@ -217,17 +231,28 @@ __global__ __launch_bounds__(256) void k_attn_p_pv(const uint16_t * __restrict__
 #pragma unroll
             for (int l = 0; l < 8; ++l) s[a][b][l] = 0.0f;
     for (int st = 0; st < nsteps; ++st) {
-        float vf[4][8], pf[4][8];
+        // the f16 operands straight into v_fma_mix (converted exactly, one rounding = fmaf of the
+        // converted values): no separate conversions
+        uint32_t vw[4][4], pw[4][4];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) unpack8(*((const uint4 *) (vl + (size_t) (4 * qd + a) * n_pad + st * 32) + r), vf[a]);
+        for (int a = 0; a < 4; ++a) {
+            const uint4 v = *((const uint4 *) (vl + (size_t) (4 * qd + a) * n_pad + st * 32) + r);
+            vw[a][0] = v.x; vw[a][1] = v.y; vw[a][2] = v.z; vw[a][3] = v.w;
+        }
 #pragma unroll
-        for (int b = 0; b < 4; ++b) unpack8(*((const uint4 *) (pl + (size_t) (4 * qt + b) * n_pad + st * 32) + r), pf[b]);
+        for (int b = 0; b < 4; ++b) {
+            const uint4 v = *((const uint4 *) (pl + (size_t) (4 * qt + b) * n_pad + st * 32) + r);
+            pw[b][0] = v.x; pw[b][1] = v.y; pw[b][2] = v.z; pw[b][3] = v.w;
+        }
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int b = 0; b < 4; ++b)
 #pragma unroll
-                for (int l = 0; l < 8; ++l) s[a][b][l] = __builtin_fmaf(vf[a][l], pf[b][l], s[a][b][l]);
+                for (int w = 0; w < 4; ++w) {
+                    s[a][b][2 * w] = fma_mix_hh<0, 0>(vw[a][w], pw[b][w], s[a][b][2 * w]);
+                    s[a][b][2 * w + 1] = fma_mix_hh<1, 1>(vw[a][w], pw[b][w], s[a][b][2 * w + 1]);
+                }
     }
     // reduce + double leftovers (ggml.c:1806-1808), in position order
     float o[4][4];
@@ -235,7 +260,7 @@ __global__ __launch_bounds__(256) void k_attn_p_pv(const uint16_t * __restrict__
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const float res = quad_reduce(s[a][b]);
+            const float res = quad_reduce_bf(s[a][b]);
             const int t = 4 * qt + b;
             const int lim = n_past + t0 + t;
             float v = res;
