@@ -377,6 +377,15 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
         }
         if (K == 13824 && epi == EPI_RESID) {
             if (cfg == 1) return go<8, 2, PRO_ACTF, EPI_RESID, 13824, 1>(P, s);
+            // deeper prefetch with 8 waves (each owns at most one row group: no cross-group prefetch)
+            if (cfg == 4) return go<8, 4, PRO_ACTF, EPI_RESID, 13824, 1>(P, s);
+            if (cfg == 5) return go<8, 5, PRO_ACTF, EPI_RESID, 13824, 1>(P, s);
+            if (cfg == 8) return go<8, 4, PRO_ACTF, EPI_RESID, 13824, 0>(P, s);
+        }
+        if (K == 5120 && epi == EPI_RESID) {
+            if (cfg == 9) return go<3, 4, PRO_ACTQ, EPI_RESID, 5120, 1>(P, s);
+            if (cfg == 10) return go<3, 5, PRO_ACTQ, EPI_RESID, 5120, 0>(P, s);
+            if (cfg == 11) return go<4, 5, PRO_ACTQ, EPI_RESID, 5120, 1>(P, s);
         }
         if (K == 5120 && epi == EPI_STORE && pro == PRO_NORM) {
             if (cfg == 3) return go<6, 5, PRO_NORM, EPI_STORE, 5120, 1>(P, s);

@@ -9,6 +9,7 @@
 #   prompt-ab    prompt A/B: super-tile width, prompt scores layout  -> r04_prompt_*.jsonl
 #   mm-probe     prompt matmul probes: knockouts, MFMA / f32 FMA issue costs
 #   attn-ab      decode attention: QKV overlap modes (parity + speed), V-slice order trace
+#   sweep13      13B Q4_1 W2 / Wo launch shapes (lib/sweep, LVK_CFG41)  -> r04_sweep13.jsonl
 #   bench        the default bench (N = 1) and rocprofv3 kernel statistics
 set -o pipefail
 mkdir -p gpurun_out
@@ -68,6 +69,13 @@ attn-ab)
   for np in 32 264 500; do
     LVK_TRACE_KIND=1 timeout -k 10 120 ./tools/probe/mv_probe_T $np > gpurun_out/attn_trace_$np.log 2>&1 || exit 5
   done ;;
+sweep13)
+  for r in 1 2; do
+    for c in 0 4 5 8 9 10 11; do
+      LVK_LIB=llama.vk_amd/lib/sweep/libllama_vk_amd.so LVK_CFG41=$c timeout -k 10 180 python3 tools/decode_speed.py 13b 64 \
+        2>/dev/null | sed "s/^{/{\"cfg41\": $c, /" | tee -a gpurun_out/r04_sweep13.jsonl || exit 4
+    done
+  done ;;
 bench)
   timeout -k 10 840 python3 bench.py > gpurun_out/r04_bench.json 2> gpurun_out/r04_bench.err
   rc=$?; tail -2 gpurun_out/r04_bench.err; [ $rc -eq 0 ] || exit $rc
@@ -80,5 +88,5 @@ bench)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o p7b \
     -- python3 $R/tools/prompt_speed.py 512 7b > $R/gpurun_out/prof/p7b.log 2>&1 || exit 5 ;;
 *)
-  echo "usage: bash tools/gpu_r04.sh suite|parity|pmc-decode|pmc-prompt|split-shm|prompt-ab|mm-probe|attn-ab|bench"; exit 2 ;;
+  echo "usage: bash tools/gpu_r04.sh suite|parity|pmc-decode|pmc-prompt|split-shm|prompt-ab|mm-probe|attn-ab|sweep13|bench"; exit 2 ;;
 esac
