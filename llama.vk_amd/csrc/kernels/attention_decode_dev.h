@@ -42,29 +42,6 @@ __device__ __forceinline__ float quad_reduce(const float s[8]) {
     return (t0 + t1) + (t2 + t3);
 }
 
-// softmax exp (exp_f16 semantics) for EM != 0 without a vector load on the common path:
-// only NaN arguments (the table covers them; softmax arguments are <= 0 otherwise) take the
-// uploaded table, behind a wave-uniform branch, so no vmcnt wait -- which would also wait
-// for the V DMA in flight -- sits in the loop
-template <int EM>
-__device__ __forceinline__ uint16_t exp_softmax(uint16_t hx, const uint16_t * __restrict__ tab, int mode) {
-    if constexpr (EM < 0) {
-        return exp_f16(hx, tab, mode);
-    } else if constexpr (EM == 0) {
-        return tab[hx];
-    } else {
-        const float x = f16_to_f32(hx);
-        uint16_t e = f32_to_f16(EM == 2 ? expf(x) : (float) exp((double) x));
-        const bool table = !(((hx & 0x8000u) || hx == 0) && (hx & 0x7fffu) <= 0x7c00u);
-        if (__builtin_amdgcn_ballot_w64(table) != 0) {
-            const uint16_t t = tab[hx];
-            e = table ? t : e;
-            asm volatile("" : "+v"(e));
-        }
-        return e;
-    }
-}
-
 
 // a workgroup barrier for LDS hand-offs only: __syncthreads() also drains vmcnt, which
 // would make every wave with V rows in flight wait for them

@@ -4,14 +4,15 @@
 // query tokens: the decode kernel's one-workgroup-per-(token, head) layout
 // re-streams K and V for every token (22 ms of a 512-token 7B prompt).
 //
-//   k_attn_p_scores  grid (H, ceil(N/T)): Q of T tokens in LDS; K streamed
-//                    once in 64-position tiles (a lane quad per position, its
-//                    K row in registers, Q broadcast from LDS); scores
-//                    KQ*scale (ggml_vec_dot_f16 order, ggml.c:1781-1815) in
-//                    LDS; -inf past n_past+t; softmax with the fp16 exp table
+//   k_attn_p_scores  grid (H, ceil(N/16)/2): a pair of mirrored 16-token
+//                    blocks per workgroup (equal causal work everywhere); Q
+//                    in LDS; K streamed in 64-position tiles (a lane per
+//                    position, its K row in registers, Q broadcast from LDS);
+//                    scores KQ*scale (ggml_vec_dot_f16 order, ggml.c:1781-1815)
+//                    in LDS; -inf past n_past+t; softmax with the fp16 exp
 //                    and the exact double sum (ggml.c:7099-7121); P rounded
 //                    to f16 -> global scratch P[h][t][n_ctx].
-//   k_attn_p_pv      grid (H, ceil(N/32), HD/32): V rows of one 32-dim slice
+//   k_attn_p_pv      grid (H, ceil(N/32), HD/32), longest blocks first: V rows of one 32-dim slice
 //                    and P of 32 tokens in LDS; each lane quad owns 4 dims x 4
 //                    tokens (16 dots, 8 AVX accumulators each); leftovers past
 //                    n_kv & ~31 in double (ggml.c:1806-1808); the slice is one
@@ -25,36 +26,20 @@
 
 #include <cstdlib>
 
+// knockout build (dev only, `make apko KO=n`, timing attribution -- wrong results): &1 the
+// score dots, &2 the softmax exp, &4 the whole softmax but the P store, &8 the P.V dots
+#ifndef LVK_ATTN_P_KO
+#define LVK_ATTN_P_KO 0
+#endif
+
 namespace lvk {
 
 namespace {
 
 constexpr int HD = 128;
 
-__device__ __forceinline__ void unpack8(const uint4 v, float f[8]) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        f[2 * k] = f16_to_f32((uint16_t) (w[k] & 0xFFFFu));
-        f[2 * k + 1] = f16_to_f32((uint16_t) (w[k] >> 16));
-    }
-}
-
-// the quad's 4 x 8 accumulators in the AVX2 F32Cx8_REDUCE order (as attention.hip)
-__device__ __forceinline__ float quad_reduce(const float s[8]) {
-    float S[8];
-#pragma unroll
-    for (int l = 0; l < 8; ++l) {
-        const float v0 = quad_bcast<0>(s[l]), v1 = quad_bcast<1>(s[l]);
-        const float v2 = quad_bcast<2>(s[l]), v3 = quad_bcast<3>(s[l]);
-        const float a = v0 + v1, b = v2 + v3;
-        S[l] = a + b;
-    }
-    const float t0 = S[0] + S[4], t1 = S[1] + S[5], t2 = S[2] + S[6], t3 = S[3] + S[7];
-    return (t0 + t1) + (t2 + t3);
-}
-
-// the same sums by two DPP butterflies: (v0 + v1) + (v2 + v3) in every lane of the quad (fp
+// the quad's 4 x 8 accumulators in the AVX2 F32Cx8_REDUCE order (lane j = AVX register j):
+// two DPP butterflies give (v0 + v1) + (v2 + v3) in every lane of the quad (fp
 // addition is commutative, so lane 1's v1 + v0 and lane 2's (v2 + v3) + (v0 + v1) are the same
 // bits) -- 4 instructions per accumulator instead of 7
 __device__ __forceinline__ float quad_reduce_bf(const float s[8]) {
@@ -70,44 +55,58 @@ __device__ __forceinline__ float quad_reduce_bf(const float s[8]) {
 }
 
 // ---------------------------------------------------------------------------
-// scores + softmax.  T query tokens per workgroup, 256 threads = 64 quads.
+// scores + softmax.  A workgroup (4 waves) owns one head and two T-token blocks, the block
+// nblk-1-y and its mirror y, one after the other: the causal 64-position tiles of the pair sum
+// to about the same count in every workgroup, so each SIMD keeps 2 busy waves to the end (a
+// VALU-bound wave alone issues at about half the rate, profiles/r04_valu_cycles.log).  Wave w
+// takes tokens w, w+4, ..; a lane owns position p = pb + lane of each tile, its K row packed in
+// 64 VGPRs with the next tile's row in flight, and runs all 32 AVX accumulators of
+// ggml_vec_dot_f16 itself with v_fma_mix (f16 operands converted exactly, one rounding), then
+// the F32Cx8 reduce in registers.  EM: the softmax exp mode (lvk_device.h exp_softmax).
 // ---------------------------------------------------------------------------
-// SV 1: a lane per position and a wave per token (4 waves: tokens w, w+4, ...): the lane keeps
-// its K row packed (64 VGPRs) and runs all 32 AVX accumulators of ggml_vec_dot_f16 itself
-// with v_fma_mix (f16 operands converted exactly, one rounding), then the F32Cx8 reduce in
-// registers -- 159 instructions per score instead of 4 lanes x ~125 (a quad per position:
-// cross-lane reduce, per-token Q conversion)
-template <int T, int SV>
+template <int T, int EM>
 __global__ __launch_bounds__(256) void k_attn_p_scores(const uint16_t * __restrict__ q16, const uint16_t * __restrict__ kc,
                                                        const uint16_t * __restrict__ exp_tab, const StepParams * sp,
                                                        int E, int n_ctx, float scale, uint16_t * __restrict__ P,
-                                                       int exp_computed) {
+                                                       int exp_mode) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int n_past = sp->n_past, N = sp->n_tokens;
     const int n_kv = n_past + N;
-    const int h = blockIdx.x, t0 = blockIdx.y * T;
-    const int nt = min(T, N - t0);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = tid & 3, quad = tid >> 2;
+    const int nblk = (N + T - 1) / T;
+    const int h = blockIdx.x;
+    // wave made visibly uniform: the token loops branch on scalars, not exec masks
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint4 * qs = (uint4 *) smem;                             // [T][16] uint4: Q rows (f16)
     float * sc = (float *) (smem + T * 256);                  // [T][n_ctx] scores, then exp values
-    const int lim_hi = n_past + t0 + nt - 1;                 // last unmasked position of the block
+    const int n_pad = (n_kv + 31) & ~31;
 
-    for (int i = tid; i < T * 16; i += 256) {
-        const int t = i >> 4;
-        qs[i] = t < nt ? *((const uint4 *) (q16 + (size_t) (t0 + t) * E + h * HD) + (i & 15)) : make_uint4(0, 0, 0, 0);
-    }
-    __syncthreads();
+    for (int ph = 0; ph < 2; ++ph) {
+        const int b = ph == 0 ? nblk - 1 - (int) blockIdx.y : (int) blockIdx.y;
+        if (ph == 1) {
+            if (b >= nblk - 1 - b) break;                   // odd block count: the middle block alone
+            __syncthreads();                                 // the first block's rows are read out
+        }
+        const int t0 = b * T;
+        const int nt = min(T, N - t0);
+        const int lim_hi = n_past + t0 + nt - 1;             // last unmasked position of the block
+        for (int i = tid; i < T * 16; i += 256) {
+            const int t = i >> 4;
+            qs[i] = t < nt ? *((const uint4 *) (q16 + (size_t) (t0 + t) * E + h * HD) + (i & 15)) : make_uint4(0, 0, 0, 0);
+        }
+        __syncthreads();
 
-    if constexpr (SV == 1) {
-        // ---- scores: lane owns position p = pb + lane of each 64-position tile, wave w tokens w, w+4, ..
-        for (int pb = 0; pb <= lim_hi; pb += 64) {
-            const int p = pb + lane;
-            const bool live = p <= lim_hi;
-            uint4 kr[16];
-            const uint4 * kp = (const uint4 *) (kc + (size_t) min(p, lim_hi) * E + h * HD);
+        auto load = [&](uint4 (&kr)[16], int pb) {
+            const uint4 * kp = (const uint4 *) (kc + (size_t) min(pb + lane, lim_hi) * E + h * HD);
 #pragma unroll
             for (int i = 0; i < 16; ++i) kr[i] = kp[i];
-            for (int t = wave; t < nt; t += 4) {
+        };
+        auto tile = [&](const uint4 (&kr)[16], int pb) {
+            const int p = pb + lane;
+            const bool live = p <= lim_hi;
+            // wave < nt: at least one token, so the first pass consumes the tile's loads and the
+            // compiler knows them done when the registers are reloaded
+            int t = wave;
+            do {
                 // accumulator (j, l) of ggml_vec_dot_f16 (ggml.c:1781-1815): elements 32 st + 8 j + l,
                 // st = 0..3 in order; uint4 4 st + j holds the 8 of (st, j), word w elements 2w, 2w + 1
                 float acc[4][8];
@@ -116,7 +115,7 @@ __global__ __launch_bounds__(256) void k_attn_p_scores(const uint16_t * __restri
 #pragma unroll
                     for (int l = 0; l < 8; ++l) acc[j][l] = 0.0f;
 #pragma unroll
-                for (int st = 0; st < 4; ++st) {
+                for (int st = 0; st < ((LVK_ATTN_P_KO & 1) ? 0 : 4); ++st) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const uint4 q = qs[t * 16 + 4 * st + j];          // wave-uniform: an LDS broadcast
@@ -129,63 +128,63 @@ __global__ __launch_bounds__(256) void k_attn_p_scores(const uint16_t * __restri
                         }
                     }
                 }
-                // F32Cx8 reduce in the order of quad_reduce (accumulator j = quad lane j there)
+                // F32Cx8 reduce: accumulator j plays the AVX register j (quad_reduce order)
                 float S[8];
 #pragma unroll
                 for (int l = 0; l < 8; ++l) {
-                    const float a = acc[0][l] + acc[1][l], b = acc[2][l] + acc[3][l];
-                    S[l] = a + b;
+                    const float a = acc[0][l] + acc[1][l], c = acc[2][l] + acc[3][l];
+                    S[l] = a + c;
                 }
                 const float t0v = S[0] + S[4], t1v = S[1] + S[5], t2v = S[2] + S[6], t3v = S[3] + S[7];
-                const float kq = (t0v + t1v) + (t2v + t3v);
+                float kq = (t0v + t1v) + (t2v + t3v);
+                if (LVK_ATTN_P_KO & 1) kq = __builtin_bit_cast(float, (kr[0].x ^ (uint32_t) t) & 0xBFFFFFFFu) * 1e-30f;
                 if (live) sc[(size_t) t * n_ctx + p] = p <= n_past + t0 + t ? kq * scale : -INFINITY;
+                t += 4;
+            } while (t < nt);
+        };
+        if (wave < nt) {
+            // tiles in pairs, the next tile's K loads always in flight (clamped to lim_hi): one
+            // loop exit, and a skipped second tile drains its loads itself, so the compiler's
+            // wait before each tile's first use counts only that tile's loads
+            uint4 ka[16], kb[16];
+            load(ka, 0);
+            for (int pb = 0; pb <= lim_hi; pb += 128) {
+                load(kb, pb + 64);
+                tile(ka, pb);
+                load(ka, pb + 128);
+                if (pb + 64 <= lim_hi) tile(kb, pb + 64);
+                else __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0)
             }
         }
-    } else
-    for (int pb = 0; pb <= lim_hi; pb += 64) {
-        const int p = pb + quad;
-        const bool live = p <= lim_hi;
-        uint4 kr[4];
-        const uint4 * kp = (const uint4 *) (kc + (size_t) min(p, lim_hi) * E + h * HD) + r;
-#pragma unroll
-        for (int st = 0; st < 4; ++st) kr[st] = kp[st * 4];
-        float kf[4][8];
-#pragma unroll
-        for (int st = 0; st < 4; ++st) unpack8(kr[st], kf[st]);
-        for (int t = 0; t < nt; ++t) {
-            float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                float qf[8];
-                unpack8(qs[t * 16 + st * 4 + r], qf);      // broadcast across quads
-#pragma unroll
-                for (int l = 0; l < 8; ++l) s[l] = __builtin_fmaf(kf[st][l], qf[l], s[l]);
-            }
-            const float kq = quad_reduce(s);
-            if (r == 0 && live) sc[(size_t) t * n_ctx + p] = p <= n_past + t0 + t ? kq * scale : -INFINITY;
-        }
-    }
-    __syncthreads();
+        __syncthreads();
 
-    // ---- softmax per token row (ggml.c:7099-7121); wave w owns rows w, w+4, ... ----
-    for (int t = wave; t < nt; t += 4) {
-        float * row = sc + (size_t) t * n_ctx;
-        const int lim = n_past + t0 + t;
-        // positions lim+1 .. n_kv-1 are -inf (ggml.c:7028-7031): max over the live ones
-        float mx = -INFINITY;
-        for (int p = lane; p <= lim; p += 64) { const float v = row[p]; mx = v > mx ? v : mx; }
-        mx = wave_max_f(mx);
-        double sum = 0.0;      // exact in any order: every term is an fp16 value in [0,1]
-        for (int p = lane; p <= lim; p += 64) {
-            const float e = f16_to_f32(exp_f16(f32_to_f16(row[p] - mx), exp_tab, exp_computed));
-            sum += (double) e;
-            row[p] = e;
+        // ---- softmax per token row (ggml.c:7099-7121); wave w owns rows w, w+4, ... ----
+        for (int t = wave; t < nt; t += 4) {
+            float * row = sc + (size_t) t * n_ctx;
+            const int lim = n_past + t0 + t;
+            // positions lim+1 .. n_kv-1 are -inf (ggml.c:7028-7031): max over the live ones
+            float mx = -INFINITY;
+            if (!(LVK_ATTN_P_KO & 4))
+                for (int p = lane; p <= lim; p += 64) { const float v = row[p]; mx = v > mx ? v : mx; }
+            mx = wave_max_f(mx);
+            double sum = 0.0;      // exact in any order: every term is an fp16 value in [0,1]
+            if (!(LVK_ATTN_P_KO & 4))
+                for (int p = lane; p <= lim; p += 64) {
+                    const float e = (LVK_ATTN_P_KO & 2) ? row[p] - mx
+                                                        : f16_to_f32(exp_softmax<EM>(f32_to_f16(row[p] - mx), exp_tab, exp_mode));
+                    sum += (double) e;
+                    row[p] = e;
+                }
+            sum = wave_sum_d(sum);
+            const float scl = (float) (1.0 / sum);
+            // P rounded to f16 (the mul_mat's src1 conversion), two positions per lane
+            uint32_t * prow = (uint32_t *) (P + ((size_t) h * N + t0 + t) * n_ctx);
+            for (int p = 2 * lane; p < n_pad; p += 128) {
+                const uint32_t lo = p <= lim ? f32_to_f16(row[p] * scl) : 0u;
+                const uint32_t hi = p + 1 <= lim ? f32_to_f16(row[p + 1] * scl) : 0u;
+                prow[p >> 1] = lo | hi << 16;
+            }
         }
-        sum = wave_sum_d(sum);
-        const float scl = (float) (1.0 / sum);
-        uint16_t * prow = P + ((size_t) h * N + t0 + t) * n_ctx;
-        const int n_pad = (n_kv + 31) & ~31;
-        for (int p = lane; p < n_pad; p += 64) prow[p] = p <= lim ? f32_to_f16(row[p] * scl) : (uint16_t) 0;
     }
 }
 
@@ -200,7 +199,8 @@ __global__ __launch_bounds__(256) void k_attn_p_pv(const uint16_t * __restrict__
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int n_past = sp->n_past, N = sp->n_tokens;
     const int n_kv = n_past + N;
-    const int h = blockIdx.x, t0 = blockIdx.y * 32, ds = blockIdx.z;
+    // the longest blocks (most causal steps) first, so the tail of the launch is short ones
+    const int h = blockIdx.x, t0 = (gridDim.y - 1 - blockIdx.y) * 32, ds = blockIdx.z;
     const int nt = min(32, N - t0);
     const int tid = threadIdx.x, r = tid & 3, quad = tid >> 2;
     const int qd = quad & 7, qt = quad >> 3;
@@ -213,13 +213,30 @@ __global__ __launch_bounds__(256) void k_attn_p_pv(const uint16_t * __restrict__
     uint16_t * pl = vl + (size_t) 32 * n_pad;                  // [32 tokens][n_pad]
     const int d0 = h * HD + ds * 32;
 
-    // stage V rows d0..d0+31 and the P rows of the block (16-byte pieces)
-    const int per = nfill / 8;
-    for (int i = tid; i < 32 * per; i += 256) {
-        const int row = i / per, c = i % per;
-        ((uint4 *) (vl + (size_t) row * n_pad))[c] = ((const uint4 *) (vc + (size_t) (d0 + row) * n_ctx))[c];
-        ((uint4 *) (pl + (size_t) row * n_pad))[c] =
-            row < nt ? ((const uint4 *) (P + ((size_t) h * N + t0 + row) * n_ctx))[c] : make_uint4(0, 0, 0, 0);
+    // stage V rows d0..d0+31 and the P rows of the block (16-byte pieces), 8 + 8 loads in
+    // flight per thread before the LDS writes
+    const int per = nfill / 8, tot = 32 * per;
+    for (int i0 = 0; i0 < tot; i0 += 256 * 8) {
+        uint4 va[8], pa[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + 256 * u + tid;
+            const int row = i / per, c = i - row * per;
+            va[u] = pa[u] = make_uint4(0, 0, 0, 0);
+            if (i < tot) {
+                va[u] = ((const uint4 *) (vc + (size_t) (d0 + row) * n_ctx))[c];
+                if (row < nt) pa[u] = ((const uint4 *) (P + ((size_t) h * N + t0 + row) * n_ctx))[c];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + 256 * u + tid;
+            const int row = i / per, c = i - row * per;
+            if (i < tot) {
+                ((uint4 *) (vl + (size_t) row * n_pad))[c] = va[u];
+                ((uint4 *) (pl + (size_t) row * n_pad))[c] = pa[u];
+            }
+        }
     }
     __syncthreads();
 
@@ -230,7 +247,7 @@ __global__ __launch_bounds__(256) void k_attn_p_pv(const uint16_t * __restrict__
         for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int l = 0; l < 8; ++l) s[a][b][l] = 0.0f;
-    for (int st = 0; st < nsteps; ++st) {
+    for (int st = 0; st < ((LVK_ATTN_P_KO & 8) ? 0 : nsteps); ++st) {
         // the f16 operands straight into v_fma_mix (converted exactly, one rounding = fmaf of the
         // converted values): no separate conversions
         uint32_t vw[4][4], pw[4][4];
@@ -357,17 +374,21 @@ hipError_t launch_attention_prompt(const AttnLaunch & A, uint16_t * p_scratch, v
     if (A.out_qtype == Q4_1 ? (xm != nullptr) != (xs41 != nullptr) : A.out_qtype != Q4_0 || xs41)
         return hipErrorNotSupported;
     const float scale = 1.0f / sqrtf((float) A.n_embd / (float) A.n_head);   // llama.cpp:1028
-    constexpr int T = 32;
+    constexpr int T = 16;
     EventSplit ev;
     ev.first();
     const size_t lds1 = (size_t) T * 256 + (size_t) T * A.n_ctx * 4;
-    static const int sv = [] { const char * e = getenv("LVK_ATTN_P_SV"); return e ? atoi(e) : 1; }();
-    if (sv == 1)
-        LVK_LAUNCH((k_attn_p_scores<T, 1>), dim3(A.n_head, (A.n_tokens + T - 1) / T), dim3(256), lds1, s, A.q16, A.kc,
-                   A.exp_tab, A.sp, A.n_embd, A.n_ctx, scale, p_scratch, A.exp_computed);
+    const int nblk = (A.n_tokens + T - 1) / T;
+    const dim3 g1(A.n_head, (nblk + 1) / 2);
+    if (A.exp_computed == 2)
+        LVK_LAUNCH((k_attn_p_scores<T, 2>), g1, dim3(256), lds1, s, A.q16, A.kc, A.exp_tab, A.sp, A.n_embd, A.n_ctx,
+                   scale, p_scratch, A.exp_computed);
+    else if (A.exp_computed == 1)
+        LVK_LAUNCH((k_attn_p_scores<T, 1>), g1, dim3(256), lds1, s, A.q16, A.kc, A.exp_tab, A.sp, A.n_embd, A.n_ctx,
+                   scale, p_scratch, A.exp_computed);
     else
-        LVK_LAUNCH((k_attn_p_scores<T, 0>), dim3(A.n_head, (A.n_tokens + T - 1) / T), dim3(256), lds1, s, A.q16, A.kc,
-                   A.exp_tab, A.sp, A.n_embd, A.n_ctx, scale, p_scratch, A.exp_computed);
+        LVK_LAUNCH((k_attn_p_scores<T, 0>), g1, dim3(256), lds1, s, A.q16, A.kc, A.exp_tab, A.sp, A.n_embd, A.n_ctx,
+                   scale, p_scratch, A.exp_computed);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds2 = (size_t) 64 * A.n_ctx * 2;

@@ -49,6 +49,29 @@ __device__ __forceinline__ uint16_t exp_f16(uint16_t hx, const uint16_t * __rest
     return tab[hx];
 }
 
+// softmax exp (exp_f16 semantics) for EM != 0 without a vector load on the common path:
+// only NaN arguments (the table covers them; softmax arguments are <= 0 otherwise) take the
+// uploaded table, behind a wave-uniform branch, so no vmcnt wait -- which would also wait
+// for loads in flight (the decode attention's V DMA) -- sits in the loop
+template <int EM>
+__device__ __forceinline__ uint16_t exp_softmax(uint16_t hx, const uint16_t * __restrict__ tab, int mode) {
+    if constexpr (EM < 0) {
+        return exp_f16(hx, tab, mode);
+    } else if constexpr (EM == 0) {
+        return tab[hx];
+    } else {
+        const float x = f16_to_f32(hx);
+        uint16_t e = f32_to_f16(EM == 2 ? expf(x) : (float) exp((double) x));
+        const bool table = !(((hx & 0x8000u) || hx == 0) && (hx & 0x7fffu) <= 0x7c00u);
+        if (__builtin_amdgcn_ballot_w64(table) != 0) {
+            const uint16_t t = tab[hx];
+            e = table ? t : e;
+            asm volatile("" : "+v"(e));
+        }
+        return e;
+    }
+}
+
 // quad_perm DPP broadcast of lane k (0..3) of each 4-lane quad
 template <int K>
 __device__ __forceinline__ float quad_bcast(float v) {

@@ -106,7 +106,7 @@ struct RopeTable {            // host-built with glibc powf/cosf/sinf (ggml.c:72
 // prologue (how the matvec obtains its quantized input)
 enum Pro : int { PRO_NORM = 0, PRO_ACTQ = 1, PRO_ACTF = 2 /* f32 input, quantize only */ };
 // epilogue (what it does with row results)
-enum Epi : int { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_SWIGLU_F32 = 4 };
+enum Epi : int { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_SWIGLU_F32 = 4, EPI_ROPE_KV = 5 };
 
 struct MvLaunch {
     QMatrix w;
@@ -271,6 +271,15 @@ hipError_t launch_mm_mfma41(const QMatrix & w, const void * xm, const void * xs,
                             const uint16_t * silu_tab, hipStream_t s);
 hipError_t launch_act41_f16(const float * x, const float * g, int N, int K, void * xm, void * xs, hipStream_t s);
 hipError_t launch_actq41_to_f16(const ActQ & q, int N, int K, void * xm, void * xs, hipStream_t s);
+// the prompt QKV matmul with RoPE + KV append in its epilogue (Q4_0, f16 KV cache): the
+// f32 Q|K|V rows never reach memory; q16 / kc / vc get exactly what launch_rope_kv writes
+struct RopeKV {
+    const float2 * rope;       // [n_ctx][hd/2] cos, sin
+    const StepParams * sp;     // n_past
+    int n_ctx, E, hd;
+    uint16_t * q16, * kc, * vc;
+};
+hipError_t launch_mm_qkv_rope(const QMatrix & w, const void * xm, const float * da, int N, const RopeKV & r, hipStream_t s);
 // RoPE + KV append of stored Q|K|V rows qkv [N][3E]
 hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 * rope, const StepParams * sp,
                           int n_ctx, uint16_t * q16, uint16_t * kc, uint16_t * vc, hipStream_t s, int kv32 = 0);

@@ -107,6 +107,7 @@ struct MmParams {
     int out_tok0;
     const uint16_t * silu_tab;
     int supertile;           // 1: super tiles of 4 row tiles (default; LVK_MM_SUPERTILE=0: row tiles)
+    RopeKV rk;               // EPI_ROPE_KV only
 };
 
 __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t o) {
@@ -145,6 +146,20 @@ template <int EPI>
 __device__ __forceinline__ void mm_store(const MmParams & P, const f32x16_t (&acc)[4], int lane, int w, int m0, int n0) {
     const int h = lane >> 5;
     const int jj = (lane >> 4) & 1;
+    // EPI_ROPE_KV: the 8 cos/sin pairs this lane needs, loaded before the reduction and any
+    // store (issued in the loop below they each wait a full latency behind a possibly
+    // aliasing store)
+    float2 cs[4][2];
+    if constexpr (EPI == EPI_ROPE_KV) {
+        const int n = n0 + (lane & 15);
+        const int pos = P.rk.sp->n_past + min(n, P.N - 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = (m0 + 32 * w + 8 * q + 4 * h) % P.rk.hd;
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) cs[q][pp] = P.rk.rope[(size_t) pos * (P.rk.hd / 2) + (e >> 1) + pp];
+        }
+    }
     float res[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -173,6 +188,37 @@ __device__ __forceinline__ void mm_store(const MmParams & P, const f32x16_t (&ac
                 }
                 const int row = m0 + 32 * w + 8 * q;
                 *(float4 *) (P.y + (size_t) (P.out_tok0 + n) * P.ldy + row / 2) = make_float4(uu[0], uu[1], uu[2], uu[3]);
+            }
+        }
+    } else if constexpr (EPI == EPI_ROPE_KV) {
+        // rows [0, E) Q, [E, 2E) K, [2E, 3E) V of token n; a wave's 32 rows lie in one of them.
+        // RoPE (ggml.c:7209-7232, as k_rope_kv) on the pairs (p, p + 1), then the f16 stores of
+        // the reference's cpy into the cache views (llama.cpp:1010-1024)
+        const RopeKV & r = P.rk;
+        if (jj == 0 && n < P.N) {
+            const int pos = r.sp->n_past + n;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = m0 + 32 * w + 8 * q + 4 * h;
+                const int which = row / r.E, e = row - which * r.E;
+                if (which < 2) {
+                    uint32_t hw[2];
+#pragma unroll
+                    for (int pp = 0; pp < 4; pp += 2) {
+                        const float x0 = res[4 * q + pp], x1 = res[4 * q + pp + 1];
+                        const float2 c = cs[q][pp >> 1];
+                        const float a0 = x0 * c.x, b0 = x1 * c.y;
+                        const float o0 = a0 - b0;
+                        const float a1 = x0 * c.y, b1 = x1 * c.x;
+                        const float o1 = a1 + b1;
+                        hw[pp >> 1] = (uint32_t) f32_to_f16(o0) | (uint32_t) f32_to_f16(o1) << 16;
+                    }
+                    uint16_t * dst = which == 0 ? r.q16 + (size_t) n * r.E + e : r.kc + (size_t) pos * r.E + e;
+                    *(uint2 *) dst = make_uint2(hw[0], hw[1]);
+                } else {
+#pragma unroll
+                    for (int pp = 0; pp < 4; ++pp) r.vc[(size_t) (e + pp) * r.n_ctx + pos] = f32_to_f16(res[4 * q + pp]);
+                }
             }
         }
     } else {
@@ -621,6 +667,23 @@ hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, 
         default: return hipErrorInvalidValue;
     }
 #undef LVK_MM_GO
+    return hipGetLastError();
+}
+
+hipError_t launch_mm_qkv_rope(const QMatrix & w, const void * xm, const float * da, int N, const RopeKV & r,
+                              hipStream_t s) {
+    if (w.qtype != Q4_0 || !mm_mfma_supported(w) || N <= 0 || w.M != 3 * r.E || r.E % 32 || r.hd % 4 || !r.sp)
+        return hipErrorInvalidValue;
+    MmParams P{};
+    P.nib = w.nib; P.scl = (const float4 *) w.scl;
+    P.M = w.M; P.K = w.K; P.nb = w.K / 32; P.NC = (P.nb + 31) / 32;
+    P.xm = (const uint2 *) xm; P.da = da; P.N = N; P.ntt = (N + TN - 1) / TN;
+    P.a16 = (const uint2 *) w.a16;
+    P.supertile = mm_supertile();
+    P.rk = r;
+    const dim3 grid((w.M / TM) * P.ntt);
+    if (P.a16) LVK_LAUNCH((k_mm_q40_mfma<EPI_ROPE_KV, true>), grid, dim3(NT), LVK_MM_BLDS ? LDS_TOTAL_BL : LDS_TOTAL, s, P);
+    else LVK_LAUNCH((k_mm_q40_mfma<EPI_ROPE_KV, false>), grid, dim3(NT), LVK_MM_BLDS ? LDS_TOTAL_BL : LDS_TOTAL, s, P);
     return hipGetLastError();
 }
 

@@ -359,10 +359,16 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
             uint16_t * kcl = kc_layer(il);
             uint16_t * vcl = vc_layer(il);
             timed_launch(K_QKV, 0, [&] { return act(x, ly.attn_norm, E); });
-            timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mm(ly.wqkv, qkv32, 3 * E, EPI_STORE, nullptr); });
-            timed_launch(K_QKV, 0, [&] {
-                return launch_rope_kv(qkv32, n, E, hd, rope, sp_d, n_ctx, q16, kcl, vcl, stream, kv32);
-            });
+            if (!q41 && !kv32 && mm_rope_fused) {
+                // RoPE + KV append in the matmul's epilogue (the f32 rows never reach memory)
+                const RopeKV rk{rope, sp_d, n_ctx, E, hd, q16, kcl, vcl};
+                timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return launch_mm_qkv_rope(ly.wqkv, xh, xda, n, rk, stream); });
+            } else {
+                timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mm(ly.wqkv, qkv32, 3 * E, EPI_STORE, nullptr); });
+                timed_launch(K_QKV, 0, [&] {
+                    return launch_rope_kv(qkv32, n, E, hd, rope, sp_d, n_ctx, q16, kcl, vcl, stream, kv32);
+                });
+            }
             AttnLaunch at{q16, kcl, vcl, scores, aq_attn, model.qtype, exp_tab, sp_d, n, E, H, n_ctx};
             at.exp_computed = exp_computed;
             at.err = err_d;

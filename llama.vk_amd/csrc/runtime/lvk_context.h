@@ -120,7 +120,9 @@ struct Context {
     uint16_t * xh = nullptr;     // masked MFMA B-fragment image of the quantized activations (mm_act_bytes)
     float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales
     void * xside = nullptr;      // Q4_1: the activations' side image (mm41_act_side_bytes)
-    float * qkv32 = nullptr;     // [C][3E] Q|K|V rows before RoPE
+    float * qkv32 = nullptr;     // [C][3E] Q|K|V rows before RoPE (Q4_1 / f32 KV prompts)
+    // Q4_0 prompt: RoPE + KV append fused into the QKV matmul (LVK_MM_ROPE=0: separate kernel)
+    bool mm_rope_fused = [] { const char * e = getenv("LVK_MM_ROPE"); return !e || atoi(e) != 0; }();
     float * uf = nullptr;        // [C][F] silu(w1 x) * (w3 x)
 
     // persistent single-token decode (decode_persistent.hip): one launch per token;

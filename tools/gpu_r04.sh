@@ -10,6 +10,8 @@
 #   mm-probe     prompt matmul probes: knockouts, MFMA / f32 FMA issue costs
 #   attn-ab      decode attention: QKV overlap modes (parity + speed), V-slice order trace
 #   sweep13      13B Q4_1 W2 / Wo launch shapes (lib/sweep, LVK_CFG41)  -> r04_sweep13.jsonl
+#   apko         prompt attention knockouts (lib/apko_<KO>) + the table exp mode, per-kernel stats
+#   attn-p       prompt attention parity (ops, paths, model, 7B full) + speed + kernel stats
 #   bench        the default bench (N = 1) and rocprofv3 kernel statistics
 set -o pipefail
 mkdir -p gpurun_out
@@ -76,6 +78,26 @@ sweep13)
         2>/dev/null | sed "s/^{/{\"cfg41\": $c, /" | tee -a gpurun_out/r04_sweep13.jsonl || exit 4
     done
   done ;;
+apko)
+  mkdir -p gpurun_out/apko
+  cd /tmp && export TMPDIR=/tmp
+  for v in base table 1 2 4 8; do
+    case $v in base) e="LVK_NONE=1";; table) e="LVK_EXP_TABLE=1";; *) e="LVK_LIB=$R/llama.vk_amd/lib/apko_$v/libllama_vk_amd.so";; esac
+    export $e
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/apko -o $v \
+      -- python3 $R/tools/prompt_speed.py 512 7b > $R/gpurun_out/apko/$v.log 2>&1 || exit 5
+    unset ${e%%=*}
+    grep -h "k_attn_p\|k_rope_kv" $R/gpurun_out/apko/${v}_kernel_stats.csv | cut -c1-60,150-230 | sed "s/^/$v /" || true
+  done ;;
+attn-p)
+  timeout -k 10 300 $T tests/test_gpu_ops.py > gpurun_out/attn_p.log 2>&1 && \
+  timeout -k 10 600 $T tests/test_gpu_attn_paths.py tests/test_gpu_model.py tests/test_gpu_7b_full.py >> gpurun_out/attn_p.log 2>&1
+  rc=$?; grep -E "passed|failed" gpurun_out/attn_p.log; [ $rc -eq 0 ] || exit $rc
+  for r in 1 2; do timeout -k 10 180 python3 tools/prompt_speed.py 512 7b 2>/dev/null | tee -a gpurun_out/attn_p.jsonl || exit 4; done
+  mkdir -p gpurun_out/attn_p
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/attn_p -o p7b \
+    -- python3 $R/tools/prompt_speed.py 512 7b > $R/gpurun_out/attn_p/p7b.log 2>&1 || exit 5 ;;
 bench)
   timeout -k 10 840 python3 bench.py > gpurun_out/r04_bench.json 2> gpurun_out/r04_bench.err
   rc=$?; tail -2 gpurun_out/r04_bench.err; [ $rc -eq 0 ] || exit $rc
@@ -88,5 +110,5 @@ bench)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o p7b \
     -- python3 $R/tools/prompt_speed.py 512 7b > $R/gpurun_out/prof/p7b.log 2>&1 || exit 5 ;;
 *)
-  echo "usage: bash tools/gpu_r04.sh suite|parity|pmc-decode|pmc-prompt|split-shm|prompt-ab|mm-probe|attn-ab|sweep13|bench"; exit 2 ;;
+  echo "usage: bash tools/gpu_r04.sh suite|parity|pmc-decode|pmc-prompt|split-shm|prompt-ab|mm-probe|attn-ab|sweep13|apko|attn-p|bench"; exit 2 ;;
 esac
