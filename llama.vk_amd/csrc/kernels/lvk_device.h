@@ -166,6 +166,15 @@ __device__ __forceinline__ size_t xm_slot(int t, int nb, int b, int c, int l) {
     return ((((size_t) (t >> 4) * nb + b) * 2 + (c >> 1)) * 64 + l) * 2 + (c & 1);
 }
 
+// token of workgroup i in a one-workgroup-per-token launch of ceil(N/128)*128 workgroups:
+// workgroup i runs on XCD i % 8, and the 16 tokens of token tile tau all go to XCD tau % 8,
+// so the 16-byte pieces they write into the same fragment-image lines (xm_slot) meet in one
+// L2 instead of being merged from 8 XCDs (>= N: no token)
+__device__ __forceinline__ int xcd_grouped_token(int i) {
+    const int tau = ((i >> 7) << 3) | (i & 7);
+    return tau * 16 + ((i >> 3) & 15);
+}
+
 // prompt-matmul tile of workgroup slot L (its XCD-contiguous index, mm_mfma.hip): row tile
 // rt, token tile tt.  Row tiles outer, token tiles inner; supertile: groups of 4 row tiles x
 // every token tile with the token tiles outer, so the 64 workgroups an XCD runs at once share

@@ -106,7 +106,7 @@ struct RopeTable {            // host-built with glibc powf/cosf/sinf (ggml.c:72
 // prologue (how the matvec obtains its quantized input)
 enum Pro : int { PRO_NORM = 0, PRO_ACTQ = 1, PRO_ACTF = 2 /* f32 input, quantize only */ };
 // epilogue (what it does with row results)
-enum Epi : int { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_SWIGLU_F32 = 4, EPI_ROPE_KV = 5 };
+enum Epi : int { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_SWIGLU_F32 = 4, EPI_ROPE_KV = 5, EPI_SWIGLU_Q = 6 };
 
 struct MvLaunch {
     QMatrix w;
@@ -280,6 +280,11 @@ struct RopeKV {
     uint16_t * q16, * kc, * vc;
 };
 hipError_t launch_mm_qkv_rope(const QMatrix & w, const void * xm, const float * da, int N, const RopeKV & r, hipStream_t s);
+// the prompt W1|W3 matmul (Q4_0) with SwiGLU and the W2 input's quantize_row_q4_0 in its
+// epilogue: writes the masked fragment image xq (mm_act_bytes(N, M/2), zeroed once) + xqda
+// directly, as launch_act_f16(silu(w1 x) * w3 x, nullptr, ...) would
+hipError_t launch_mm_w13_q(const QMatrix & w, const void * xm, const float * da, int N, const uint16_t * silu_tab,
+                           void * xq, float * xqda, hipStream_t s);
 // RoPE + KV append of stored Q|K|V rows qkv [N][3E]
 hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 * rope, const StepParams * sp,
                           int n_ctx, uint16_t * q16, uint16_t * kc, uint16_t * vc, hipStream_t s, int kv32 = 0);

@@ -108,6 +108,9 @@ struct MmParams {
     const uint16_t * silu_tab;
     int supertile;           // 1: super tiles of 4 row tiles (default; LVK_MM_SUPERTILE=0: row tiles)
     RopeKV rk;               // EPI_ROPE_KV only
+    uint2 * xq;              // EPI_SWIGLU_Q: the W2 input's fragment image, scales, blocks per token
+    float * xqda;
+    int nbq;
 };
 
 __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t o) {
@@ -189,6 +192,48 @@ __device__ __forceinline__ void mm_store(const MmParams & P, const f32x16_t (&ac
                 const int row = m0 + 32 * w + 8 * q;
                 *(float4 *) (P.y + (size_t) (P.out_tok0 + n) * P.ldy + row / 2) = make_float4(uu[0], uu[1], uu[2], uu[3]);
             }
+        }
+    } else if constexpr (EPI == EPI_SWIGLU_Q) {
+        // SwiGLU as EPI_SWIGLU_F32, then quantize_row_q4_0 of the W2 input (ggml.c:621-685, the
+        // arithmetic of k_act_q40_f16_tile) straight into its fragment image: the wave's 16
+        // outputs (features m0/2 + 16w ..) are half of Q4_0 block b, the other half in wave
+        // w ^ 1, the amax exchanged through LDS (free after the main loop's last barrier)
+        extern __shared__ __attribute__((aligned(16))) uint8_t smem_e[];
+        float uu[16];
+        float am = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float o = __shfl_xor(res[i], 32);
+            const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res[i])]);    // ggml.c:2495
+            uu[i] = sl * o;                                                  // llama.cpp:1096
+            const float a = fabsf(uu[i]);
+            am = a > am ? a : am;
+        }
+        __syncthreads();
+        float * red = (float *) smem_e;
+        if (jj == 0 && h == 0) red[w * 16 + (lane & 15)] = am;
+        __syncthreads();
+        if (jj == 0 && h == 0 && n < P.N) {
+            const float ao = red[(w ^ 1) * 16 + (lane & 15)];
+            const float amax = (w & 1) ? (am > ao ? am : ao) : (ao > am ? ao : am);
+            const float d = amax / 7.0f;                              // ggml.c:651
+            const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;     // ggml.c:653
+            const int b = ((m0 >> 1) + 16 * w) >> 5;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t hh[4];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const int qv = ((int) __builtin_rintf(uu[4 * q + p] * id) + 8) & 15;   // ggml.c:655-684
+                    hh[p] = __builtin_bit_cast(uint16_t, (_Float16) (float) (qv - 8));
+                }
+                // elements 16 (w & 1) + 4q + p of the block: group c = 2 (w & 1) + q / 2, its
+                // first half (q even) in lane n, its second in lane 48 + n (k_act_q40_f16 order)
+                const int c = 2 * (w & 1) + (q >> 1);
+                P.xq[xm_slot(n, P.nbq, b, c, (q & 1) ? 48 + (n & 15) : (n & 15))] =
+                    make_uint2(hh[0] | hh[2] << 16, hh[1] | hh[3] << 16);
+            }
+            if ((w & 1) == 0) P.xqda[(size_t) n * P.nbq + b] = d;
         }
     } else if constexpr (EPI == EPI_ROPE_KV) {
         // rows [0, E) Q, [E, 2E) K, [2E, 3E) V of token n; a wave's 32 rows lie in one of them.
@@ -468,10 +513,11 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
 // ---------------------------------------------------------------------------
 template <bool NORM>
 __global__ __launch_bounds__(256) void k_act_q40_f16(const float * __restrict__ x, const float * __restrict__ g,
-                                                     int K, uint2 * __restrict__ xm, float * __restrict__ da) {
+                                                     int N, int K, uint2 * __restrict__ xm, float * __restrict__ da) {
     __shared__ double red[4];
     __shared__ float s_scale;
-    const int t = blockIdx.x;
+    const int t = xcd_grouped_token(blockIdx.x);
+    if (t >= N) return;
     const int tid = threadIdx.x;
     const int nunits = K / 8;
     const float * xr = x + (size_t) t * K;
@@ -540,6 +586,51 @@ __global__ __launch_bounds__(256) void k_act_q40_f16(const float * __restrict__ 
                 make_uint2(h[4] | (uint32_t) h[6] << 16, h[5] | (uint32_t) h[7] << 16);
             if ((u & 3) == 0) da[(size_t) t * (K / 32) + (u >> 2)] = d;
         }
+    }
+}
+
+// The quantizer without RMSNorm (the W2 input) by token tiles: a wave takes one 32-block b of
+// the tile's 16 tokens (lane quad = token, lane = 8 values), so each of its two stores fills
+// whole 256-byte runs of the fragment image (lanes 0-15 | 48-63 of chain pair c/2) instead of
+// 16-byte pieces of lines the other 15 tokens' workgroups -- on other XCDs -- also write
+// (14 us per 512 x 11008 activation that way).  Same arithmetic per block as k_act_q40_f16.
+__global__ __launch_bounds__(256) void k_act_q40_f16_tile(const float * __restrict__ x, int N, int K,
+                                                          uint2 * __restrict__ xm, float * __restrict__ da) {
+    const int nb = K / 32;
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (b >= nb) return;                                     // wave-uniform; no barriers below
+    const int tl = lane >> 2, c = lane & 3;
+    const int t = blockIdx.x * 16 + tl;
+    const bool live = t < N;
+    float v[8];
+    if (live) {
+        const float * xp = x + (size_t) t * K + b * 32 + c * 8;
+        const float4 a = *(const float4 *) xp, bb = *(const float4 *) (xp + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = bb.x; v[5] = bb.y; v[6] = bb.z; v[7] = bb.w;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 0.0f;
+    }
+    float amax = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float a = fabsf(v[e]); amax = a > amax ? a : amax; }
+    const float o0 = quad_bcast<0>(amax), o1 = quad_bcast<1>(amax);
+    const float o2 = quad_bcast<2>(amax), o3 = quad_bcast<3>(amax);
+    const float m01 = o1 > o0 ? o1 : o0, m23 = o3 > o2 ? o3 : o2;
+    amax = m23 > m01 ? m23 : m01;
+    const float d = amax / 7.0f;                              // ggml.c:651
+    const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;     // ggml.c:653
+    if (live) {
+        uint16_t h[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int q = ((int) __builtin_rintf(v[e] * id) + 8) & 15;   // ggml.c:655-684
+            h[e] = __builtin_bit_cast(uint16_t, (_Float16) (float) (q - 8));
+        }
+        xm[xm_slot(t, nb, b, c, tl)] = make_uint2(h[0] | (uint32_t) h[2] << 16, h[1] | (uint32_t) h[3] << 16);
+        xm[xm_slot(t, nb, b, c, 48 + tl)] = make_uint2(h[4] | (uint32_t) h[6] << 16, h[5] | (uint32_t) h[7] << 16);
+        if (c == 0) da[(size_t) t * nb + b] = d;
     }
 }
 
@@ -687,10 +778,32 @@ hipError_t launch_mm_qkv_rope(const QMatrix & w, const void * xm, const float * 
     return hipGetLastError();
 }
 
+hipError_t launch_mm_w13_q(const QMatrix & w, const void * xm, const float * da, int N, const uint16_t * silu_tab,
+                           void * xq, float * xqda, hipStream_t s) {
+    if (w.qtype != Q4_0 || !mm_mfma_supported(w) || N <= 0 || w.M % 64 || !silu_tab || !xq || !xqda)
+        return hipErrorInvalidValue;
+    MmParams P{};
+    P.nib = w.nib; P.scl = (const float4 *) w.scl;
+    P.M = w.M; P.K = w.K; P.nb = w.K / 32; P.NC = (P.nb + 31) / 32;
+    P.xm = (const uint2 *) xm; P.da = da; P.N = N; P.ntt = (N + TN - 1) / TN;
+    P.a16 = (const uint2 *) w.a16;
+    P.supertile = mm_supertile();
+    P.silu_tab = silu_tab;
+    P.xq = (uint2 *) xq; P.xqda = xqda; P.nbq = w.M / 64;
+    const dim3 grid((w.M / TM) * P.ntt);
+    if (P.a16) LVK_LAUNCH((k_mm_q40_mfma<EPI_SWIGLU_Q, true>), grid, dim3(NT), LVK_MM_BLDS ? LDS_TOTAL_BL : LDS_TOTAL, s, P);
+    else LVK_LAUNCH((k_mm_q40_mfma<EPI_SWIGLU_Q, false>), grid, dim3(NT), LVK_MM_BLDS ? LDS_TOTAL_BL : LDS_TOTAL, s, P);
+    return hipGetLastError();
+}
+
 hipError_t launch_act_f16(const float * x, const float * g, int N, int K, void * xm, float * da, hipStream_t s) {
     if (K % 256 || N <= 0) return hipErrorInvalidValue;
-    if (g) LVK_LAUNCH(k_act_q40_f16<true>, dim3(N), dim3(256), 0, s, x, g, K, (uint2 *) xm, da);
-    else LVK_LAUNCH(k_act_q40_f16<false>, dim3(N), dim3(256), 0, s, x, g, K, (uint2 *) xm, da);
+    static const bool tile = [] { const char * e = getenv("LVK_ACT_TILE"); return !e || atoi(e) != 0; }();
+    const dim3 gt((unsigned) ((N + 127) / 128 * 128));   // k_act_q40_f16: XCD-grouped token order
+    if (g) LVK_LAUNCH(k_act_q40_f16<true>, gt, dim3(256), 0, s, x, g, N, K, (uint2 *) xm, da);
+    else if (tile)
+        LVK_LAUNCH(k_act_q40_f16_tile, dim3((N + 15) / 16, (K / 32 + 3) / 4), dim3(256), 0, s, x, N, K, (uint2 *) xm, da);
+    else LVK_LAUNCH(k_act_q40_f16<false>, gt, dim3(256), 0, s, x, g, N, K, (uint2 *) xm, da);
     return hipGetLastError();
 }
 

@@ -353,11 +353,12 @@ __global__ __launch_bounds__(NT, OCC41) void k_mm_q41_dma(Mm41Params P) {
 // quantize_row_q4_1 (AVX2 branch, ggml.c:847-920; matvec_common.h q41_quad) -> the
 // fragment and side images.  One workgroup per token, one lane quad per block.
 template <bool NORM>
-__global__ __launch_bounds__(256) void k_act_q41_f16(const float * __restrict__ x, const float * __restrict__ g, int K,
-                                                     uint4 * __restrict__ xm, uint4 * __restrict__ xs) {
+__global__ __launch_bounds__(256) void k_act_q41_f16(const float * __restrict__ x, const float * __restrict__ g, int N,
+                                                     int K, uint4 * __restrict__ xm, uint4 * __restrict__ xs) {
     __shared__ double red[4];
     __shared__ float s_scale;
-    const int t = blockIdx.x;
+    const int t = xcd_grouped_token(blockIdx.x);
+    if (t >= N) return;
     const int tid = threadIdx.x;
     const int nunits = K / 8;
     const float * xr = x + (size_t) t * K;
@@ -513,8 +514,9 @@ hipError_t launch_mm_mfma41(const QMatrix & w, const void * xm, const void * xs,
 
 hipError_t launch_act41_f16(const float * x, const float * g, int N, int K, void * xm, void * xs, hipStream_t s) {
     if (K % 256 || N <= 0) return hipErrorInvalidValue;
-    if (g) LVK_LAUNCH(k_act_q41_f16<true>, dim3(N), dim3(256), 0, s, x, g, K, (uint4 *) xm, (uint4 *) xs);
-    else LVK_LAUNCH(k_act_q41_f16<false>, dim3(N), dim3(256), 0, s, x, g, K, (uint4 *) xm, (uint4 *) xs);
+    const dim3 gt((unsigned) ((N + 127) / 128 * 128));   // XCD-grouped token order
+    if (g) LVK_LAUNCH(k_act_q41_f16<true>, gt, dim3(256), 0, s, x, g, N, K, (uint4 *) xm, (uint4 *) xs);
+    else LVK_LAUNCH(k_act_q41_f16<false>, gt, dim3(256), 0, s, x, g, N, K, (uint4 *) xm, (uint4 *) xs);
     return hipGetLastError();
 }
 

@@ -119,6 +119,12 @@ void Context::init(const llama_context_params & p) {
         LVK_HIP(hipMemset(xh, 0, mm_act_bytes((int) Cp, (int) KX)));   // masked slots stay zero
         xda = (float *) model.alloc(Cp * (KX / 32) * 4);
         if (model.qtype == Q4_1) xside = model.alloc(mm41_act_side_bytes((int) Cp, (int) KX));
+        const char * sq = getenv("LVK_MM_SWIGLU_Q");
+        if (model.qtype == Q4_0 && (!sq || atoi(sq) != 0)) {
+            xh2 = (uint16_t *) model.alloc(mm_act_bytes((int) Cp, (int) F));
+            LVK_HIP(hipMemset(xh2, 0, mm_act_bytes((int) Cp, (int) F)));   // masked slots stay zero
+            xda2 = (float *) model.alloc(Cp * (F / 32) * 4);
+        }
         qkv32 = (float *) model.alloc(C * 3 * E * 4);
         uf = (float *) model.alloc(C * F * 4);
         prompt_exact = getenv("LVK_PROMPT_EXACT") && atoi(getenv("LVK_PROMPT_EXACT")) != 0;
@@ -388,9 +394,19 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
             }
             timed_launch(K_WO, qbytes(ly.wo), [&] { return mm(ly.wo, x, E, EPI_RESID, nullptr); });
             timed_launch(K_W13, 0, [&] { return act(x, ly.ffn_norm, E); });
-            timed_launch(K_W13, qbytes(ly.w13), [&] { return mm(ly.w13, uf, F, EPI_SWIGLU_F32, silu_tab); });
-            timed_launch(K_W2, 0, [&] { return act(uf, nullptr, F); });
-            timed_launch(K_W2, qbytes(ly.w2), [&] { return mm(ly.w2, x, E, EPI_RESID, nullptr); });
+            if (!q41 && xh2) {
+                // SwiGLU + the W2 input's quantization in the W1|W3 epilogue
+                timed_launch(K_W13, qbytes(ly.w13), [&] {
+                    return launch_mm_w13_q(ly.w13, xh, xda, n, silu_tab, xh2, xda2, stream);
+                });
+                timed_launch(K_W2, qbytes(ly.w2), [&] {
+                    return launch_mm_mfma(ly.w2, xh2, xda2, n, x, E, 0, EPI_RESID, nullptr, stream);
+                });
+            } else {
+                timed_launch(K_W13, qbytes(ly.w13), [&] { return mm(ly.w13, uf, F, EPI_SWIGLU_F32, silu_tab); });
+                timed_launch(K_W2, 0, [&] { return act(uf, nullptr, F); });
+                timed_launch(K_W2, qbytes(ly.w2), [&] { return mm(ly.w2, x, E, EPI_RESID, nullptr); });
+            }
         }
         if (!model.has_head || !head) return;
         if (last_only || !mm_mfma_supported(model.output)) {

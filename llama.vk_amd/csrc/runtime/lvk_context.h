@@ -119,6 +119,10 @@ struct Context {
     int attn_mode() const;
     uint16_t * xh = nullptr;     // masked MFMA B-fragment image of the quantized activations (mm_act_bytes)
     float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales
+    // Q4_0 prompt: the W2 input image written by the W1|W3 epilogue (EPI_SWIGLU_Q; the W1|W3
+    // launch still reads xh); LVK_MM_SWIGLU_Q=0: f32 uf + k_act_q40_f16_tile instead
+    uint16_t * xh2 = nullptr;
+    float * xda2 = nullptr;
     void * xside = nullptr;      // Q4_1: the activations' side image (mm41_act_side_bytes)
     float * qkv32 = nullptr;     // [C][3E] Q|K|V rows before RoPE (Q4_1 / f32 KV prompts)
     // Q4_0 prompt: RoPE + KV append fused into the QKV matmul (LVK_MM_ROPE=0: separate kernel)

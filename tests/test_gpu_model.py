@@ -223,17 +223,19 @@ def test_mfma_prompt_chunks_match_reference_golden(lvk, tiny_models, name):
     m.close()
 
 
-@pytest.mark.parametrize("a16,rope", [("1", "1"), ("0", "1"), ("1", "0")])
-def test_mfma_prompt_7b_shaped_vs_oracle(lvk, oracle, model_dir, monkeypatch, a16, rope):
+@pytest.mark.parametrize("a16,rope,swq", [("1", "1", "1"), ("0", "1", "1"), ("1", "0", "0")])
+def test_mfma_prompt_7b_shaped_vs_oracle(lvk, oracle, model_dir, monkeypatch, a16, rope, swq):
     """LLaMA-7B layer shapes (K = 4096 / 11008, 32 heads), 2 layers, a 200-token prompt (ragged
     last token tile) through the MFMA matmuls -- A operands from the f16 A-fragment images
     (default) or unpacked from the nibble images (LVK_PROMPT_A16=0); RoPE + KV append in the QKV
-    matmul's epilogue (default) or by k_rope_kv (LVK_MM_ROPE=0) -- then decode on the KV cache
-    it wrote"""
+    matmul's epilogue (default) or by k_rope_kv (LVK_MM_ROPE=0); the W2 input quantized in the
+    W1|W3 epilogue (default) or by k_act_q40_f16_tile (LVK_MM_SWIGLU_Q=0) -- then decode on the
+    KV cache it wrote"""
     from oracle_lib import gen_model
     path = gen_model(os.path.join(model_dir, "w4096_l2.bin"), n_embd=4096, n_head=32, n_layer=2, ftype=2, seed=7)
     monkeypatch.setenv("LVK_PROMPT_A16", a16)
     monkeypatch.setenv("LVK_MM_ROPE", rope)
+    monkeypatch.setenv("LVK_MM_SWIGLU_Q", swq)
     m = lvk.Llama(path, n_ctx=512)
     om = oracle.model(path, 512)
     toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 200)], np.int32)
