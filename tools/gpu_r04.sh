@@ -12,6 +12,7 @@
 #   sweep13      13B Q4_1 W2 / Wo launch shapes (lib/sweep, LVK_CFG41)  -> r04_sweep13.jsonl
 #   apko         prompt attention knockouts (lib/apko_<KO>) + the table exp mode, per-kernel stats
 #   attn-p       prompt attention parity (ops, paths, model, 7B full) + speed + kernel stats
+#   attn-d       decode attention parity (ops, paths, beside, seq wrap, 7B full) + 7B decode speed
 #   bench        the default bench (N = 1) and rocprofv3 kernel statistics
 set -o pipefail
 mkdir -p gpurun_out
@@ -98,6 +99,12 @@ attn-p)
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/attn_p -o p7b \
     -- python3 $R/tools/prompt_speed.py 512 7b > $R/gpurun_out/attn_p/p7b.log 2>&1 || exit 5 ;;
+attn-d)
+  timeout -k 10 300 $T tests/test_gpu_ops.py > gpurun_out/attn_d.log 2>&1 && \
+  timeout -k 10 700 $T tests/test_gpu_attn_paths.py tests/test_gpu_attn_beside.py tests/test_gpu_seq_wrap.py \
+    tests/test_gpu_7b_full.py tests/test_gpu_decode_chain.py >> gpurun_out/attn_d.log 2>&1
+  rc=$?; grep -E "passed|failed" gpurun_out/attn_d.log; [ $rc -eq 0 ] || exit $rc
+  for r in 1 2; do timeout -k 10 180 python3 tools/decode_speed.py 7b 96 2>/dev/null | tee -a gpurun_out/attn_d.jsonl || exit 4; done ;;
 bench)
   timeout -k 10 840 python3 bench.py > gpurun_out/r04_bench.json 2> gpurun_out/r04_bench.err
   rc=$?; tail -2 gpurun_out/r04_bench.err; [ $rc -eq 0 ] || exit $rc
@@ -110,5 +117,5 @@ bench)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o p7b \
     -- python3 $R/tools/prompt_speed.py 512 7b > $R/gpurun_out/prof/p7b.log 2>&1 || exit 5 ;;
 *)
-  echo "usage: bash tools/gpu_r04.sh suite|parity|pmc-decode|pmc-prompt|split-shm|prompt-ab|mm-probe|attn-ab|sweep13|apko|attn-p|bench"; exit 2 ;;
+  echo "usage: bash tools/gpu_r04.sh suite|parity|pmc-decode|pmc-prompt|split-shm|prompt-ab|mm-probe|attn-ab|sweep13|apko|attn-p|attn-d|bench"; exit 2 ;;
 esac
