@@ -267,8 +267,9 @@ size_t mm41_side_bytes(int M, int K);
 size_t mm41_act_side_bytes(int N, int K);
 hipError_t launch_build_mm41(const QMatrix & w, void * a16, void * side, hipStream_t s);
 bool mm_mfma41_supported(const QMatrix & w);
+struct RopeKV;
 hipError_t launch_mm_mfma41(const QMatrix & w, const void * xm, const void * xs, int N, float * y, int ldy, int epi,
-                            const uint16_t * silu_tab, hipStream_t s);
+                            const uint16_t * silu_tab, hipStream_t s, const RopeKV * rk = nullptr);   // rk: EPI_ROPE_KV
 hipError_t launch_act41_f16(const float * x, const float * g, int N, int K, void * xm, void * xs, hipStream_t s);
 hipError_t launch_actq41_to_f16(const ActQ & q, int N, int K, void * xm, void * xs, hipStream_t s);
 // the prompt QKV matmul with RoPE + KV append in its epilogue (Q4_0, f16 KV cache): the

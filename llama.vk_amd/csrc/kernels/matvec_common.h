@@ -2,6 +2,7 @@
 // (activation table in LDS, reference Q4_0 quantizer pieces, octet reduce).
 #pragma once
 #include "lvk_device.h"
+#include "lvk_kernels.h"
 
 namespace lvk {
 namespace mv {
@@ -248,4 +249,46 @@ __device__ __forceinline__ void qkv_epilogue(float res, int row, int j, int E, i
 }
 
 }  // namespace mv
+// the RoPE + KV epilogue of a prompt-matmul lane (mm_mfma.hip, mm_mfma41.hip): the lane holds
+// rows m0 + 32w + 8q + 4h + p (p = 0..3) of token n; rows [0, E) Q, [E, 2E) K, [2E, 3E) V.
+// rope_kv_cs loads the 8 cos / sin pairs (before the reduction and any store: issued between
+// stores they each wait a full latency), rope_kv_store does RoPE (ggml.c:7209-7232, as
+// k_rope_kv) and the f16 stores of the cache views (llama.cpp:1010-1024)
+__device__ __forceinline__ void rope_kv_cs(const RopeKV & r, int N, int n, int h, int w, int m0, float2 (&cs)[4][2]) {
+    const int pos = r.sp->n_past + (n < N ? n : N - 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int e = (m0 + 32 * w + 8 * q + 4 * h) % r.hd;
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) cs[q][pp] = r.rope[(size_t) pos * (r.hd / 2) + (e >> 1) + pp];
+    }
+}
+__device__ __forceinline__ void rope_kv_store(const RopeKV & r, const float (&res)[16], const float2 (&cs)[4][2], int n,
+                                              int h, int w, int m0) {
+    const int pos = r.sp->n_past + n;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = m0 + 32 * w + 8 * q + 4 * h;
+        const int which = row / r.E, e = row - which * r.E;
+        if (which < 2) {
+            uint32_t hw[2];
+#pragma unroll
+            for (int pp = 0; pp < 4; pp += 2) {
+                const float x0 = res[4 * q + pp], x1 = res[4 * q + pp + 1];
+                const float2 c = cs[q][pp >> 1];
+                const float a0 = x0 * c.x, b0 = x1 * c.y;
+                const float o0 = a0 - b0;
+                const float a1 = x0 * c.y, b1 = x1 * c.x;
+                const float o1 = a1 + b1;
+                hw[pp >> 1] = (uint32_t) f32_to_f16(o0) | (uint32_t) f32_to_f16(o1) << 16;
+            }
+            uint16_t * dst = which == 0 ? r.q16 + (size_t) n * r.E + e : r.kc + (size_t) pos * r.E + e;
+            *(uint2 *) dst = make_uint2(hw[0], hw[1]);
+        } else {
+#pragma unroll
+            for (int pp = 0; pp < 4; ++pp) r.vc[(size_t) (e + pp) * r.n_ctx + pos] = f32_to_f16(res[4 * q + pp]);
+        }
+    }
+}
+
 }  // namespace lvk

@@ -149,20 +149,8 @@ template <int EPI>
 __device__ __forceinline__ void mm_store(const MmParams & P, const f32x16_t (&acc)[4], int lane, int w, int m0, int n0) {
     const int h = lane >> 5;
     const int jj = (lane >> 4) & 1;
-    // EPI_ROPE_KV: the 8 cos/sin pairs this lane needs, loaded before the reduction and any
-    // store (issued in the loop below they each wait a full latency behind a possibly
-    // aliasing store)
-    float2 cs[4][2];
-    if constexpr (EPI == EPI_ROPE_KV) {
-        const int n = n0 + (lane & 15);
-        const int pos = P.rk.sp->n_past + min(n, P.N - 1);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = (m0 + 32 * w + 8 * q + 4 * h) % P.rk.hd;
-#pragma unroll
-            for (int pp = 0; pp < 2; ++pp) cs[q][pp] = P.rk.rope[(size_t) pos * (P.rk.hd / 2) + (e >> 1) + pp];
-        }
-    }
+    float2 cs[4][2];                                  // EPI_ROPE_KV: cos / sin (rope_kv_cs)
+    if constexpr (EPI == EPI_ROPE_KV) rope_kv_cs(P.rk, P.N, n0 + (lane & 15), h, w, m0, cs);
     float res[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -236,36 +224,8 @@ __device__ __forceinline__ void mm_store(const MmParams & P, const f32x16_t (&ac
             if ((w & 1) == 0) P.xqda[(size_t) n * P.nbq + b] = d;
         }
     } else if constexpr (EPI == EPI_ROPE_KV) {
-        // rows [0, E) Q, [E, 2E) K, [2E, 3E) V of token n; a wave's 32 rows lie in one of them.
-        // RoPE (ggml.c:7209-7232, as k_rope_kv) on the pairs (p, p + 1), then the f16 stores of
-        // the reference's cpy into the cache views (llama.cpp:1010-1024)
-        const RopeKV & r = P.rk;
-        if (jj == 0 && n < P.N) {
-            const int pos = r.sp->n_past + n;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int row = m0 + 32 * w + 8 * q + 4 * h;
-                const int which = row / r.E, e = row - which * r.E;
-                if (which < 2) {
-                    uint32_t hw[2];
-#pragma unroll
-                    for (int pp = 0; pp < 4; pp += 2) {
-                        const float x0 = res[4 * q + pp], x1 = res[4 * q + pp + 1];
-                        const float2 c = cs[q][pp >> 1];
-                        const float a0 = x0 * c.x, b0 = x1 * c.y;
-                        const float o0 = a0 - b0;
-                        const float a1 = x0 * c.y, b1 = x1 * c.x;
-                        const float o1 = a1 + b1;
-                        hw[pp >> 1] = (uint32_t) f32_to_f16(o0) | (uint32_t) f32_to_f16(o1) << 16;
-                    }
-                    uint16_t * dst = which == 0 ? r.q16 + (size_t) n * r.E + e : r.kc + (size_t) pos * r.E + e;
-                    *(uint2 *) dst = make_uint2(hw[0], hw[1]);
-                } else {
-#pragma unroll
-                    for (int pp = 0; pp < 4; ++pp) r.vc[(size_t) (e + pp) * r.n_ctx + pos] = f32_to_f16(res[4 * q + pp]);
-                }
-            }
-        }
+        // RoPE + the f16 q / K / V stores (rope_kv_store); a wave's 32 rows lie in one of Q, K, V
+        if (jj == 0 && n < P.N) rope_kv_store(P.rk, res, cs, n, h, w, m0);
     } else {
         if (jj == 0 && n < P.N) {
 #pragma unroll

@@ -64,6 +64,7 @@ struct Mm41Params {
     int ldy;
     const uint16_t * silu_tab;
     int supertile;           // mm_tile order (mm_mfma.hip)
+    RopeKV rk;               // EPI_ROPE_KV only
 };
 
 struct Blk {                 // one block's operands of one lane
@@ -76,6 +77,8 @@ __device__ __forceinline__ void epilogue41(const Mm41Params & P, const f32x16_t 
                                            int lane, int w, int m0, int n0) {
     // AVX2 horizontal order (ggml.c:2250-2256) as in mm_mfma.hip, then + off * 32 (QK)
     const int jj = (lane >> 4) & 1, h = lane >> 5;
+    float2 cs[4][2];                                  // EPI_ROPE_KV: cos / sin (rope_kv_cs)
+    if constexpr (EPI == EPI_ROPE_KV) rope_kv_cs(P.rk, P.N, n0 + (lane & 15), h, w, m0, cs);
     float res[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -103,6 +106,8 @@ __device__ __forceinline__ void epilogue41(const Mm41Params & P, const f32x16_t 
                 *(float4 *) (P.y + (size_t) n * P.ldy + row / 2) = make_float4(uu[0], uu[1], uu[2], uu[3]);
             }
         }
+    } else if constexpr (EPI == EPI_ROPE_KV) {
+        if (jj == 0 && n < P.N) rope_kv_store(P.rk, res, cs, n, h, w, m0);
     } else {
         if (jj == 0 && n < P.N) {
 #pragma unroll
@@ -485,9 +490,13 @@ bool mm_mfma41_supported(const QMatrix & w) {
 }
 
 hipError_t launch_mm_mfma41(const QMatrix & w, const void * xm, const void * xs, int N, float * y, int ldy, int epi,
-                            const uint16_t * silu_tab, hipStream_t s) {
-    if (!mm_mfma41_supported(w) || N <= 0) return hipErrorInvalidValue;
+                            const uint16_t * silu_tab, hipStream_t s, const RopeKV * rk) {
+    if (!mm_mfma41_supported(w) || N <= 0 || (epi == EPI_ROPE_KV) != (rk != nullptr)) return hipErrorInvalidValue;
     Mm41Params P{};
+    if (rk) {
+        if (w.M != 3 * rk->E || rk->E % 32 || rk->hd % 4 || !rk->sp) return hipErrorInvalidValue;
+        P.rk = *rk;
+    }
     P.a16 = (const uint4 *) w.a16; P.side = (const uint4 *) w.side;
     P.xm = (const uint4 *) xm; P.xs = (const uint4 *) xs;
     P.M = w.M; P.nb = w.K / 32; P.N = N; P.ntt = (N + TN - 1) / TN;
@@ -506,6 +515,7 @@ hipError_t launch_mm_mfma41(const QMatrix & w, const void * xm, const void * xs,
         case EPI_STORE: LVK_MM41_GO(EPI_STORE); break;
         case EPI_RESID: LVK_MM41_GO(EPI_RESID); break;
         case EPI_SWIGLU_F32: LVK_MM41_GO(EPI_SWIGLU_F32); break;
+        case EPI_ROPE_KV: LVK_MM41_GO(EPI_ROPE_KV); break;
         default: return hipErrorInvalidValue;
     }
 #undef LVK_MM41_GO

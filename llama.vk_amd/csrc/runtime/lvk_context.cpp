@@ -365,10 +365,13 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
             uint16_t * kcl = kc_layer(il);
             uint16_t * vcl = vc_layer(il);
             timed_launch(K_QKV, 0, [&] { return act(x, ly.attn_norm, E); });
-            if (!q41 && !kv32 && mm_rope_fused) {
+            if (!kv32 && mm_rope_fused) {
                 // RoPE + KV append in the matmul's epilogue (the f32 rows never reach memory)
                 const RopeKV rk{rope, sp_d, n_ctx, E, hd, q16, kcl, vcl};
-                timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return launch_mm_qkv_rope(ly.wqkv, xh, xda, n, rk, stream); });
+                timed_launch(K_QKV, qbytes(ly.wqkv), [&] {
+                    return q41 ? launch_mm_mfma41(ly.wqkv, xh, xside, n, nullptr, 0, EPI_ROPE_KV, nullptr, stream, &rk)
+                               : launch_mm_qkv_rope(ly.wqkv, xh, xda, n, rk, stream);
+                });
             } else {
                 timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mm(ly.wqkv, qkv32, 3 * E, EPI_STORE, nullptr); });
                 timed_launch(K_QKV, 0, [&] {

@@ -124,8 +124,8 @@ struct Context {
     uint16_t * xh2 = nullptr;
     float * xda2 = nullptr;
     void * xside = nullptr;      // Q4_1: the activations' side image (mm41_act_side_bytes)
-    float * qkv32 = nullptr;     // [C][3E] Q|K|V rows before RoPE (Q4_1 / f32 KV prompts)
-    // Q4_0 prompt: RoPE + KV append fused into the QKV matmul (LVK_MM_ROPE=0: separate kernel)
+    float * qkv32 = nullptr;     // [C][3E] Q|K|V rows before RoPE (f32-KV prompts, LVK_MM_ROPE=0)
+    // prompt: RoPE + KV append fused into the QKV matmul (LVK_MM_ROPE=0: separate kernel)
     bool mm_rope_fused = [] { const char * e = getenv("LVK_MM_ROPE"); return !e || atoi(e) != 0; }();
     float * uf = nullptr;        // [C][F] silu(w1 x) * (w3 x)
 

@@ -253,23 +253,26 @@ def test_mfma_prompt_7b_shaped_vs_oracle(lvk, oracle, model_dir, monkeypatch, a1
     om.close()
 
 
-@pytest.mark.parametrize("n_ctx", [256, 2048])
-def test_mfma_prompt_13b_q4_1_shaped_vs_oracle(lvk, oracle, model_dir, n_ctx):
+@pytest.mark.parametrize("n_ctx,rope", [(256, "1"), (2048, "1"), (256, "0")])
+def test_mfma_prompt_13b_q4_1_shaped_vs_oracle(lvk, oracle, model_dir, monkeypatch, n_ctx, rope):
     """LLaMA-13B layer shapes in Q4_1 (K = 5120 / 13824, 40 heads), 2 layers: a 100-token
     prompt (ragged token tile) through the Q4_1 MFMA matmuls (mm_mfma41.hip), then decode on
     the KV cache it wrote, bit-exact against the oracle.  The Wo input comes from the prompt
     attention's fused Q4_1 epilogue (n_ctx 256) or from the generic attention's ActQ via
-    launch_actq41_to_f16 (n_ctx 2048, past the prompt attention's LDS window)"""
+    launch_actq41_to_f16 (n_ctx 2048, past the prompt attention's LDS window); RoPE + KV append
+    in the QKV matmul's epilogue (default) or by k_rope_kv (LVK_MM_ROPE=0)"""
     from oracle_lib import gen_model
     path = gen_model(os.path.join(model_dir, "w5120_l2_q41.bin"), n_embd=5120, n_head=40, n_layer=2, ftype=3, seed=11)
+    monkeypatch.setenv("LVK_MM_ROPE", rope)
     m = lvk.Llama(path, n_ctx=n_ctx)
     om = oracle.model(path, n_ctx)
     toks = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, 100)], np.int32)
     m.set_profiling(True)
     m.reset_profile()
     a = m.eval(toks, 0)
-    # the MFMA path ran: activation image, matmul and RoPE/KV launches in the QKV class per layer
-    assert m.profile()["qkv"]["launches"] == 6
+    # the MFMA path ran: activation image and matmul (+ the RoPE/KV kernel unless it is the
+    # matmul's epilogue) in the QKV class per layer
+    assert m.profile()["qkv"]["launches"] == (4 if rope == "1" else 6)
     m.set_profiling(False)
     b = om.eval(toks, 0)
     assert np.array_equal(bits(a), bits(b))
