@@ -10,7 +10,7 @@
 #   mm-probe     prompt matmul probes: knockouts, MFMA / f32 FMA issue costs
 #   attn-ab      decode attention: QKV overlap modes (parity + speed), V-slice order trace
 #   sweep13      13B Q4_1 W2 / Wo launch shapes (lib/sweep, LVK_CFG41)  -> r04_sweep13.jsonl
-#   apko         prompt attention knockouts (lib/apko_<KO>) + the table exp mode, per-kernel stats
+#   apko         prompt attention knockouts (lib/apko_<KO>: make -C llama.vk_amd apko first) + table exp
 #   attn-p       prompt attention parity (ops, paths, model, 7B full) + speed + kernel stats
 #   attn-d       decode attention parity (ops, paths, beside, seq wrap, 7B full) + 7B decode speed
 #   bench        the default bench (N = 1) and rocprofv3 kernel statistics
