@@ -88,9 +88,8 @@ LVK_API void lvk_host_tables(uint16_t * exp_tab, uint16_t * silu_tab);
 
 /* decode-step profiling of a llama_context: when enabled, every eval records
  * HIP events around each kernel class (0 embed, 1 qkv, 2 attention, 3 wo,
- * 4 w1|w3, 5 w2, 6 lm_head, 7 attention+wo, 8 the persistent decode kernel)
- * and accumulates device ms, launches and
- * algorithmic weight bytes. */
+ * 4 w1|w3, 5 w2, 6 lm_head) and accumulates device ms, launches and algorithmic
+ * weight bytes. */
 struct llama_context;
 LVK_API void lvk_set_profiling(struct llama_context * ctx, int on);
 LVK_API int lvk_get_profile(struct llama_context * ctx, double * ms, long * launches, double * bytes, int n);
@@ -103,19 +102,6 @@ LVK_API size_t lvk_weight_bytes(struct llama_context * ctx);
 LVK_API void lvk_set_prompt_exact(struct llama_context * ctx, int on);
 /* 1 = replay the captured decode graph for single-token evals (default), 0 = eager */
 LVK_API void lvk_set_graph(struct llama_context * ctx, int on);
-/* single-token decode path: 1 = the persistent one-launch-per-token kernel
- * (decode_persistent.hip, where the model shape is compiled in), 0 = one launch per
- * phase (the default; env LVK_DECODE_PERSISTENT=1 makes 1 the default) */
-LVK_API void lvk_set_decode_persistent(struct llama_context * ctx, int on);
-/* 1 when the next single-token eval of ctx runs the persistent kernel */
-LVK_API int lvk_decode_persistent_active(struct llama_context * ctx);
-/* how ctx's single-token evals run each layer's decode attention: 0 = its own launch after
- * QKV (default), 1 = beside the QKV launch on a second stream (env LVK_ATTN_BESIDE=1), 2 =
- * inside the QKV launch (env LVK_QKV_ATTN=1, 7B shapes).  1 and 2 hand the new q / k / v rows
- * over as tagged granules; each is chosen at context creation only where the workgroups of
- * both roles are guaranteed co-resident (else 0) */
-LVK_API int lvk_attn_mode(struct llama_context * ctx);
-
 /* On-device greedy sampling.  lvk_eval_greedy(ctx, token, n_past)
  * is llama_eval(ctx, &token, 1, n_past, .) followed by
  * llama_sample_top_p_top_k(ctx, ., ., ., ., temp <= 0) (llama.cpp:1703-1719,
@@ -130,7 +116,7 @@ LVK_API int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past);
  * cache ends in the same state.  The steps run as back-to-back replays of one decode graph
  * whose last kernel advances the step block and writes the next embedding row on the device,
  * so nothing crosses PCIe between steps.  n_past + n_steps <= n_ctx.  Returns 0, or -1 on
- * error (layer splits, logits_all contexts and the opt-in persistent kernel refuse it).
+ * error (layer splits and logits_all contexts refuse it).
  * The host logits of llama_get_logits are NOT refreshed. */
 LVK_API int lvk_decode_greedy(struct llama_context * ctx, int token, int n_past, int n_steps, int * out_tokens);
 /* On-device sampling: lvk_eval_sample(ctx, token, n_past, last_n, n_last,
@@ -224,10 +210,6 @@ LVK_API int lvk_stage_step(struct llama_context * ctx, const int * tokens, int n
  * pages are uploaded again by the next call.  0 / -1. */
 LVK_API int lvk_ggml_stats(uint64_t * out, int n);
 LVK_API int lvk_ggml_invalidate(const void * p, size_t n);
-
-/* 1 when this build carries the parked kernels (lib/dev: the persistent decode kernel,
- * the fused attention + Wo launch), 0 for the product library */
-LVK_API int lvk_dev_kernels(void);
 
 /* The layer split behind llama.h, one process driving n_stages HIP
  * devices: stage s holds layers [s*L/S, (s+1)*L/S) on devices[s].  llama_eval /

@@ -28,22 +28,9 @@ struct EventSplit {
     ~EventSplit() { g_launch_events = saved; }
 };
 
-// resource footprint of the kernel a launcher would start (g_footprint set: LVK_LAUNCH records
-// it instead of launching; used to check that two launches can be resident together)
-struct KernelFootprint {
-    int threads = 0;            // per workgroup
-    int vgprs = 0;              // per lane (architected + accumulation registers)
-    size_t lds = 0;             // per workgroup, static + dynamic
-    int workgroups = 0;
-};
-extern thread_local KernelFootprint * g_footprint;
-void record_footprint(const void * fn, dim3 grid, dim3 block, size_t lds);
-
 #define LVK_LAUNCH(kern, grid, block, lds, stream, ...)                                                        \
     do {                                                                                                       \
-        if (::lvk::g_footprint)                                                                                \
-            ::lvk::record_footprint(reinterpret_cast<const void *>(kern), grid, block, lds);                   \
-        else if (::lvk::g_launch_events.start || ::lvk::g_launch_events.stop)                                  \
+        if (::lvk::g_launch_events.start || ::lvk::g_launch_events.stop)                                  \
             hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ::lvk::g_launch_events.start,                \
                                   ::lvk::g_launch_events.stop, 0, __VA_ARGS__);                                \
         else                                                                                                   \
@@ -127,8 +114,6 @@ struct MvLaunch {
     RopeTable rope{};
     int n_embd = 0, head_dim = 0, n_ctx = 0;
     int kv32 = 0;                    // f32 KV cache and f32 queries (f16_kv = false)
-    unsigned long long * qkv_gran = nullptr;   // decode (matvec_cu*): also publish the q / k / v rows
-    unsigned qkv_epoch = 0;                    // as granules tagged qkv_epoch + (seq << 7) (see AttnLaunch)
     // EPI_SWIGLU
     const uint16_t * silu_tab = nullptr;   // 64Ki fp16 table
     ActQ out_q;                            // quantized u = silu(w1 x) * (w3 x)
@@ -170,11 +155,6 @@ struct AttnLaunch {
     unsigned * err = nullptr; // host-mapped error word (DevError); kernels that spin report a timeout here
     int kv32 = 0;             // f32 K, V and queries (f16_kv = false): launch_attention only
     int seq_epochs = 0;       // decode attention: granule epoch = (sp->seq << 7) + epoch (no per-token zeroing)
-    // decode attention beside QKV: the new position's q / k / v come from these granules
-    // ([3][E/2], written by the QKV launch running at the same time, MvLaunch::qkv_gran),
-    // not from q16 / kc / vc; needs seq_epochs
-    const unsigned long long * qkv_gran = nullptr;
-    size_t lds_min = 0;       // decode attention: request at least this much LDS (caps workgroups per CU)
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
 // prompt batches (N > 1, Q4_0 / Q4_1 output): scores+softmax per (head, 32 tokens) then
@@ -189,28 +169,13 @@ hipError_t launch_attention_prompt(const AttnLaunch & A, uint16_t * p_scratch, v
 // reproduces the host table exactly
 hipError_t exp_check(const uint16_t * exp_tab, int * bad_d, hipStream_t s);
 // single-token attention, 4 workgroups per head in one launch (attention_decode.hip):
-// the head's scores are exchanged through `gran` (attention_decode_scratch_bytes,
-// ZEROED before the first layer of every token) tagged with `epoch` (layer + 1,
-// never 0).  Needs A.n_tokens == 1.
+// the head's scores are exchanged through `gran` (attention_decode_scratch_bytes, zeroed
+// at allocation) tagged with `epoch` (layer + 1, never 0) + (sp->seq << 7) when
+// A.seq_epochs is set (else the scratch must be zeroed before every token).  Needs
+// A.n_tokens == 1.
 bool attention_decode_supported(int n_embd, int n_head, int n_ctx);
 size_t attention_decode_scratch_bytes(int n_head, int n_ctx);
 hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned epoch, hipStream_t s);
-// QKV (the CU-balanced matvec with the RoPE / KV epilogue, L.qkv_gran set) and the decode
-// attention of the same layer in one launch (matvec_cu.hip k_qkv_attn; 7B shapes, Q4_0):
-// cnt / cons are [H] counters QKV_CNT_STRIDE words apart (one 128-B line each: the
-// agent-scope atomics of different heads must not share a line), zero at the first launch
-// and left zero by each launch
-constexpr int QKV_CNT_STRIDE = 32;
-bool qkv_attn_supported(const QMatrix & w, int n_embd, int n_head, int n_ctx);
-hipError_t launch_qkv_attn(const MvLaunch & L, const AttnLaunch & A, void * gran, unsigned epoch, unsigned * cnt,
-                           unsigned * cons, hipStream_t s);
-// the same attention + the Wo matvec + residual add (y += Wo attn) in ONE launch
-// (attention_decode.hip, k_attn_wo): Q4_0 Wo with K = 4096 and every workgroup
-// resident (n_ctx <= 1024 here); the attention output reaches the Wo workgroups
-// as tagged granules in `gran` (same scratch and zeroing as launch_attention_decode)
-bool attention_wo_supported(int n_embd, int n_head, int n_ctx, const QMatrix & wo);
-hipError_t launch_attention_wo(const AttnLaunch & A, const QMatrix & wo, float * y, void * gran, unsigned epoch,
-                               hipStream_t s);
 
 // one-time weight repack: file-layout rows (ggml blocks) -> quad-sliced image
 // interleave4: src_rows holds two (M/2)-row matrices A then B; the image
@@ -294,60 +259,6 @@ hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 
 hipError_t launch_quantize_act(const float * x, int N, int K, int qtype, ActQ out, hipStream_t s);
 // the reference's scalar quantize_row_q4_0/1_reference (roundf, id = 1/d)
 hipError_t launch_quantize_ref(const float * x, int N, int K, int qtype, ActQ out, hipStream_t s);
-
-// ---------------------------------------------------------------------------
-// Persistent single-token decode (decode_persistent.hip): the whole forward pass of
-// one token as ONE launch of one workgroup per CU, the weight stream running ahead of
-// every dependency through an LDS ring.  Q4_0 layer matrices only.
-struct DecodeLayer {            // device-resident table, one entry per layer
-    const uint4 * nib[4];       // octet images: 0 Wq|Wk|Wv, 1 Wo, 2 W1|W3, 3 W2
-    const float4 * scl[4];
-    const float * attn_norm;
-    const float * ffn_norm;
-    uint16_t * kc;              // this layer's K cache [n_ctx][E]
-    uint16_t * vc;              // and V cache [E][n_ctx]
-};
-struct DecodeArgs {
-    const DecodeLayer * layers;
-    int n_layer, n_embd, n_ff, n_head, n_ctx, n_vocab;
-    const uint4 * out_nib;      // lm_head image (nullptr: not the last pipeline stage)
-    const float4 * out_scl;
-    const float * out_norm;
-    const void * tok_emb;       // token embeddings, file layout (xin == nullptr)
-    int emb_type;
-    const float * xin;          // stage input x [E] (nullptr: the token's embedding row)
-    float * xout;               // stage output x [E] (may be nullptr)
-    const StepParams * sp;      // n_past, token (pad0)
-    float * logits;             // [V]
-    // exchange buffers (device), one slice per layer (X: two): the published residual
-    // stream [2L][E], silu(w1 x) * w3 x [L][F], this token's q | k | v rows f16 [L][3E],
-    // the quantized attention output [L][E/32]
-    float * X;
-    float * U;
-    uint16_t * cur;
-    float * aq_d;
-    uint4 * aq_qs;
-    const uint16_t * exp_tab;
-    int exp_mode;
-    const uint16_t * silu_tab;
-    const float2 * rope;        // [n_ctx][64] {cos, sin}
-    unsigned * err;             // host-mapped error word
-    // filled by launch_decode_persistent
-    unsigned * ctr;
-    unsigned long long * gran;
-    float scale;
-    int xres_rows, act_bytes, l_act, l_att, l_ring_att, n_attn_wg;
-};
-bool decode_persistent_supported(int n_embd, int n_ff, int n_head, int n_ctx, int n_vocab, int qtype);
-// floats of the per-layer attention-output scale slices (each on its own 256-byte lines)
-size_t decode_persistent_aq_d_floats(int n_embd, int n_layer);
-// counters + score granules, zeroed by the launcher before every launch
-size_t decode_persistent_scratch_bytes(int n_head, int n_ctx);
-// fill the layout fields and the scratch pointers; false when the shape is not compiled in
-bool decode_persistent_prepare(DecodeArgs & A, void * scratch, int n_cu);
-// memset of the scratch + n_cu workgroups (one per CU, all resident: the kernel's LDS
-// admits one per CU) reading the prepared arguments from A_dev (a device copy of A)
-hipError_t launch_decode_persistent(const DecodeArgs & A, const DecodeArgs * A_dev, int n_cu, hipStream_t s);
 
 }  // namespace lvk
 

@@ -216,13 +216,10 @@ __device__ __forceinline__ uint32_t wsum_word(uint32_t w, bool other, uint32_t s
 
 // QKV epilogue of both decode matvecs, per output row (lane row r of an 8-row group, chain
 // lane j): RoPE mode 0 on q and k (ggml.c:7209-7223; rows e and e^1 are lanes l and l^8),
-// the q row / K-cache row / V-cache column stores (llama.cpp:996-1008).  gran != nullptr:
-// also the tagged granules the decode attention takes when it runs beside this launch
-// (attention_decode.hip, QB): [3][E/2] x {ep, f16(e) | f16(e + 1) << 16}, one relaxed
-// agent-scope 8-byte store per row pair (written through to memory, never in a stale L2).
+// the q row / K-cache row / V-cache column stores (llama.cpp:996-1008).
 __device__ __forceinline__ void qkv_epilogue(float res, int row, int j, int E, int hd, int pos,
                                              const float2 * rope, uint16_t * q16, uint16_t * kc, uint16_t * vc,
-                                             int n_ctx, int kv32, unsigned long long * gran, unsigned ep) {
+                                             int n_ctx, int kv32) {
     const int which = row / E;              // 0 q, 1 k, 2 v (uniform per wave: E % 8 == 0)
     const int e = row - which * E;
     const float other = __shfl_xor(res, 8);   // row e^1 lives in lanes of row r^1
@@ -237,14 +234,6 @@ __device__ __forceinline__ void qkv_epilogue(float res, int row, int j, int E, i
         if (which == 0)      kv_store(q16, e, out, kv32);
         else if (which == 1) kv_store(kc, (size_t) pos * E + e, out, kv32);
         else                 kv_store(vc, (size_t) e * n_ctx + pos, out, kv32);
-    }
-    if (gran) {
-        const float po = __shfl_xor(out, 8);
-        if (j == 0 && (e & 1) == 0) {
-            const unsigned pair = (unsigned) f32_to_f16(out) | ((unsigned) f32_to_f16(po) << 16);
-            __hip_atomic_store(gran + (size_t) which * (E / 2) + (e >> 1), ((unsigned long long) ep << 32) | pair,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 

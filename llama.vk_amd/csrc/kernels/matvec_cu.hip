@@ -20,7 +20,6 @@
 #include "lvk_device.h"
 #include "lvk_kernels.h"
 #include "matvec_common.h"
-#include "attention_decode_dev.h"
 
 namespace lvk {
 
@@ -55,9 +54,6 @@ struct CuParams {
     int n_embd, head_dim, n_ctx;
     int kv32;                   // f32 KV cache and queries (f16_kv = false)
     const uint16_t * silu_tab;
-    unsigned long long * qkv_gran;   // EPI_QKV: also publish q / k / v granules (nullptr: no)
-    unsigned qkv_epoch;             // their tag base (layer + 1; + seq << 7)
-    unsigned * qkv_cnt;             // merged launch: per-head count of finished row groups (nullptr: no)
 };
 
 // per-wave block-scale table s = dw * dx in LDS (two buffers, 8 rows x 32 blocks): the row
@@ -65,8 +61,7 @@ struct CuParams {
 // the 64 and the per-row broadcast float4 reads are bank-conflict free
 constexpr int SRS = 40, SPL = 8 * SRS;
 
-// the workgroup body (bid of nwg workgroups); k_mv_cu below, and the QKV role of the merged
-// QKV + attention launch (qkv_attn.hip)
+// the workgroup body (bid of nwg workgroups)
 template <int NW, int NP, int D, int PRO, int EPI, int KT, int PF>
 __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, const int nwg, uint8_t * smem) {
     constexpr int PT = NP * 64;                 // prologue threads
@@ -452,17 +447,7 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
             if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
         } else if constexpr (EPI == EPI_QKV) {
             const StepParams * sp = P.sp;
-            const unsigned ep = P.qkv_gran ? P.qkv_epoch + (sp->seq << 7) : 0u;
-            qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32,
-                         P.qkv_gran, ep);
-            if (P.qkv_cnt) {
-                // the merged launch: this row group counts into its head once the wave's granule
-                // stores have drained (written through, agent scope: MI355X_MICROARCH.md hand-off form)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const int e0 = grp * 8 - (grp * 8 / P.n_embd) * P.n_embd;
-                if (lane == 0)
-                    __hip_atomic_fetch_add(P.qkv_cnt + (e0 / P.head_dim) * QKV_CNT_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32);
         } else if constexpr (EPI == EPI_SWIGLU_F32) {
             // fused W1|W3 image interleaved per 4 rows: rows 0-3 of the group are
             // w1 rows 4grp..4grp+3, rows 4-7 the w3 rows (llama.cpp:1085-1096)
@@ -493,36 +478,6 @@ template <int NW, int NP, int D, int PRO, int EPI, int KT, int PF>
 __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     mv_cu_run<NW, NP, D, PRO, EPI, KT, PF>(P, blockIdx.x, gridDim.x, smem);
-}
-
-// QKV and the decode attention of one layer in ONE launch (LVK_QKV_ATTN): one workgroup per
-// CU (its LDS request is over half a CU's), 12 waves.  Waves 0-7 are the QKV matvec
-// (k_mv_cu<8, 0, 2, NORM, QKV, KT, 5>, the decode shape of 7B), which also publishes the new
-// q / k / v rows as tagged granules and counts its finished row groups per head.  Waves 8-11 of
-// the first 4 H workgroups are the decode attention of one 32-dim slice (the 4 slices of a
-// head on one XCD): they put the KV rows of positions < n_past in flight, join the QKV
-// prologue's two workgroup barriers, wait for their head's 48 row groups and read q / k / v
-// from the granules; from there they synchronise among themselves only (GroupBarrier), so the
-// QKV waves never wait on them.  Every wave is resident from the start (grid = CUs), every wait
-// is bounded.  Removes the QKV -> attention boundary and overlaps the attention's launch and
-// KV loads with the QKV stream.
-constexpr size_t qkv_attn_qlds(int KT) { return (size_t) (KT / 32) * 32 + ((KT / 32 + 31) / 32) * 128 + 8 * 2 * SPL * 4 + 8 * 8; }
-constexpr int QKV_ATTN_HW_BARRIERS = 2;    // mv_cu_run<.., NP 0, PRO_NORM, ..>: the RMS sum, the table
-
-template <int KT, int QT, int EM>
-__global__ __launch_bounds__(768) void k_qkv_attn(CuParams P, AttnDArgs A, int nh4, int exp) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if (threadIdx.x < 512) {
-        mv_cu_run<8, 0, 2, PRO_NORM, EPI_QKV, KT, 5>(P, blockIdx.x, gridDim.x, smem);
-        return;
-    }
-    const int b = blockIdx.x, tid = (int) threadIdx.x - 512;
-    if (b >= nh4 || (exp & 1)) {     // (exp & 1: A/B probe, LVK_QKV_ATTN_EXP -- the QKV role alone)
-        for (int i = 0; i < QKV_ATTN_HW_BARRIERS; ++i) __builtin_amdgcn_s_barrier();
-        return;
-    }
-    const int h = (b & 7) + 8 * (b >> 5), sl = (b >> 3) & 3;
-    attn_d_run<QT, EM, true, true, true>(A, h, sl, smem + qkv_attn_qlds(KT), tid, tid == 0, QKV_ATTN_HW_BARRIERS);
 }
 
 // -- host -------------------------------------------------------------------
@@ -597,8 +552,6 @@ CuParams cu_params(const MvLaunch & L) {
     P.q16 = L.q16; P.kc = L.kc; P.vc = L.vc; P.rope = L.rope.cs;
     P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx; P.kv32 = L.kv32;
     P.silu_tab = L.silu_tab;
-    P.qkv_gran = L.qkv_gran;
-    P.qkv_epoch = L.qkv_epoch;
     return P;
 }
 }  // namespace
@@ -668,53 +621,6 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         if (epi == EPI_STORE && pro == PRO_NORM) return go<4, 0, 2, PRO_NORM, EPI_STORE, 22016>(P, s);
     }
     return hipErrorNotSupported;
-}
-
-// the merged QKV + decode attention launch (k_qkv_attn); hipErrorNotSupported where it does
-// not apply (the caller then launches the two kernels)
-static size_t qkv_attn_lds(int n_ctx) {
-    return std::max(qkv_attn_qlds(4096) + attn_lds(n_ctx), (size_t) 80 * 1024 + 256);   // one workgroup per CU
-}
-
-bool qkv_attn_supported(const QMatrix & w, int n_embd, int n_head, int n_ctx) {
-    if (w.qtype != Q4_0 || w.K != 4096 || w.M != 3 * n_embd || n_embd != 4096) return false;
-    if (!attention_decode_supported(n_embd, n_head, n_ctx) || n_head % 8) return false;
-    if (4 * n_head > cu_count() || w.M / 8 < cu_count()) return false;
-    if (qkv_attn_lds(n_ctx) > 160 * 1024) return false;
-    static const bool regs_ok = [] {
-        hipFuncAttributes a{};
-        if (hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_qkv_attn<4096, Q4_0, 0>)) != hipSuccess) return false;
-        return a.numRegs <= 168 && a.sharedSizeBytes == 0;     // 12 waves: 3 per SIMD
-    }();
-    return regs_ok;
-}
-
-hipError_t launch_qkv_attn(const MvLaunch & L, const AttnLaunch & A, void * gran, unsigned epoch, unsigned * cnt,
-                           unsigned * cons, hipStream_t s) {
-    if (!qkv_attn_supported(L.w, L.n_embd, A.n_head, A.n_ctx) || L.n_tokens != 1 || A.n_tokens != 1 || !cnt || !cons ||
-        !L.qkv_gran || !A.seq_epochs || A.out_qtype != Q4_0 || epoch == 0)
-        return hipErrorNotSupported;
-    CuParams P = cu_params(L);
-    P.qkv_cnt = cnt;
-    AttnDArgs a = attn_args(A, gran, epoch);
-    a.qkv_gran = L.qkv_gran;
-    a.qkv_cnt = cnt;
-    a.qkv_cons = cons;
-    a.qkv_target = 3 * (L.head_dim / 8);     // q, k and v row groups of a head
-    a.qkv_consumers = 4;                     // attention slices per head
-    const dim3 grid(cu_count());
-    const size_t lds = qkv_attn_lds(A.n_ctx);
-    const int nh4 = 4 * A.n_head;
-    // A/B probe bits (LVK_QKV_ATTN_EXP): 1 the attention waves leave at once (timing only),
-    // 2 no row-group counters (the attention polls the granules themselves)
-    static const int exp = [] { const char * e = getenv("LVK_QKV_ATTN_EXP"); return e ? atoi(e) : 0; }();
-    if (exp & 2) { P.qkv_cnt = nullptr; a.qkv_cnt = nullptr; }
-    switch (a.exp_mode) {
-        case 2: LVK_LAUNCH((k_qkv_attn<4096, Q4_0, 2>), grid, dim3(768), lds, s, P, a, nh4, exp); break;
-        case 1: LVK_LAUNCH((k_qkv_attn<4096, Q4_0, 1>), grid, dim3(768), lds, s, P, a, nh4, exp); break;
-        default: LVK_LAUNCH((k_qkv_attn<4096, Q4_0, 0>), grid, dim3(768), lds, s, P, a, nh4, exp); break;
-    }
-    return hipGetLastError();
 }
 
 }  // namespace lvk

@@ -44,8 +44,6 @@ struct Cu41Params {
     int n_embd, head_dim, n_ctx;
     int kv32;                   // f32 KV cache and queries (f16_kv = false)
     const uint16_t * silu_tab;
-    unsigned long long * qkv_gran;   // EPI_QKV: also publish q / k / v granules (nullptr: no)
-    unsigned qkv_epoch;             // their tag base (layer + 1; + seq << 7)
 };
 
 // per-wave block-product tables in LDS: 4 tables (s, dx*my, mx*dy, mx*my) of 8 rows x 32
@@ -292,9 +290,7 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
             if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
         } else if constexpr (EPI == EPI_QKV) {
             const StepParams * sp = P.sp;
-            const unsigned ep = P.qkv_gran ? P.qkv_epoch + (sp->seq << 7) : 0u;
-            qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32,
-                         P.qkv_gran, ep);
+            qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32);
         } else if constexpr (EPI == EPI_SWIGLU_F32) {
             // fused W1|W3 image interleaved per 4 rows: rows 0-3 of the group are
             // w1 rows 4grp..4grp+3, rows 4-7 the w3 rows (llama.cpp:1085-1096)
@@ -357,8 +353,6 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
     P.q16 = L.q16; P.kc = L.kc; P.vc = L.vc; P.rope = L.rope.cs;
     P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx; P.kv32 = L.kv32;
     P.silu_tab = L.silu_tab;
-    P.qkv_gran = L.qkv_gran;
-    P.qkv_epoch = L.qkv_epoch;
     const int K = L.w.K;
 #ifdef LVK_PROBE_SWEEP   // dev probe builds only: LVK_CFG41 selects a launch shape (waves, prefetch depth)
     {

@@ -7,16 +7,6 @@
 
 namespace lvk {
 thread_local LaunchEvents g_launch_events;
-thread_local KernelFootprint * g_footprint = nullptr;
-
-void record_footprint(const void * fn, dim3 grid, dim3 block, size_t lds) {
-    hipFuncAttributes a{};
-    if (hipFuncGetAttributes(&a, fn) != hipSuccess) { *g_footprint = KernelFootprint{}; return; }
-    g_footprint->threads = (int) (block.x * block.y * block.z);
-    g_footprint->vgprs = a.numRegs;
-    g_footprint->lds = a.sharedSizeBytes + lds;
-    g_footprint->workgroups = (int) (grid.x * grid.y * grid.z);
-}
 
 namespace {
 

@@ -210,7 +210,7 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q41_mfma(Mm41Params P) {
 
 // ---------------------------------------------------------------------------
 // The same matmul with the operands streamed through a per-wave LDS ring by LDS-DMA
-// (global_load_lds_dwordx4, the decode_persistent.hip recipe).  hipcc's waitcnt pass
+// (global_load_lds_dwordx4).  hipcc's waitcnt pass
 // puts a vmcnt(0) at the register-ring loop's header (the refill issued last in a trip
 // is waited for at once); the DMAs are invisible to it, so the wave keeps RS blocks in
 // flight and waits with its own count.  Per wave RS slots of 6 x 1 KiB (a16 pair halves,

@@ -13,6 +13,7 @@
 #include <ctime>
 #include <csignal>
 #include <execinfo.h>
+#include <fcntl.h>
 #include <queue>
 #include <sys/mman.h>
 #include <unistd.h>
@@ -322,6 +323,15 @@ static void segv_trace(int sig, siginfo_t * si, void *) {
     if (n > 0) (void) !write(2, buf, (size_t) n);
     void * fr[64];
     backtrace_symbols_fd(fr, backtrace(fr, 64), 2);
+    // the mappings, so unsymbolized frames and the faulting address can be placed
+    // (open / read / write only: async-signal-safe)
+    const int fd = open("/proc/self/maps", O_RDONLY);
+    if (fd >= 0) {
+        (void) !write(2, "/proc/self/maps:\n", 17);
+        char mb[4096];
+        for (ssize_t r; (r = read(fd, mb, sizeof(mb))) > 0;) (void) !write(2, mb, (size_t) r);
+        close(fd);
+    }
     signal(sig, SIG_DFL);
     raise(sig);
 }

@@ -2,7 +2,7 @@
 //
 // The reference builds a ~1253-node ggml graph per token and runs it on a CPU
 // thread pool (llama.cpp:927-1137, ggml.c:9230-9651).  Here the same forward
-// pass is 6 fused kernels per layer (+ embedding and lm_head) on one stream:
+// pass is 5 fused kernels per layer (+ embedding and lm_head) on one stream:
 //   QKV matvec  (rms_norm*g -> Q4 quantize -> Wq|Wk|Wv -> RoPE -> KV append)
 //   attention   (scores; softmax -> P.V -> Q4 quantize of the merged heads)
 //   Wo matvec   (+ residual)
@@ -76,9 +76,6 @@ Context::~Context() {
     if (sp_h) (void) hipHostFree(sp_h);
     if (tok_h) (void) hipHostFree(tok_h);
     if (err_h) (void) hipHostFree(err_h);
-    if (ev_fork) (void) hipEventDestroy(ev_fork);
-    if (ev_join) (void) hipEventDestroy(ev_join);
-    if (side) (void) hipStreamDestroy(side);
     if (stream) (void) hipStreamDestroy(stream);
 }
 
@@ -129,66 +126,12 @@ void Context::init(const llama_context_params & p) {
         uf = (float *) model.alloc(C * F * 4);
         prompt_exact = getenv("LVK_PROMPT_EXACT") && atoi(getenv("LVK_PROMPT_EXACT")) != 0;
         old_attention = getenv("LVK_ATTN_V1") && atoi(getenv("LVK_ATTN_V1")) != 0;
-        fuse_attn_wo = getenv("LVK_FUSE_ATTN_WO") && atoi(getenv("LVK_FUSE_ATTN_WO")) != 0;
         attn_gran = model.alloc(attention_decode_scratch_bytes((int) H, (int) C));
         LVK_HIP(hipMemset(attn_gran, 0, attention_decode_scratch_bytes((int) H, (int) C)));
         // granule tags (seq << 7) + layer + 1 stay unique per token with up to 126 layers
-        seq_epochs = !fuse_attn_wo && L <= 126;
-        // the decode attention beside QKV: every QKV workgroup and the 4 H attention workgroups
-        // are resident together (one QKV workgroup per CU, the attention's LDS beside it), the
-        // granule waits are bounded (error word) -- LVK_ATTN_BESIDE=1
-        attn_beside = seq_epochs && !kv32 && attention_decode_supported((int) E, (int) H, (int) C) &&
-                      matvec_cu_supported((int) E, model.qtype) && getenv("LVK_ATTN_BESIDE") &&
-                      atoi(getenv("LVK_ATTN_BESIDE")) != 0 && beside_fits();
-        qkv_attn = seq_epochs && !kv32 && !attn_beside && model.qtype == Q4_0 && !model.layers.empty() &&
-                   qkv_attn_supported(model.layers[0].wqkv, (int) E, (int) H, (int) C) && getenv("LVK_QKV_ATTN") &&
-                   atoi(getenv("LVK_QKV_ATTN")) != 0;
-        if (attn_beside || qkv_attn) {
-            qkv_gran = (unsigned long long *) model.alloc(3 * (E / 2) * 8);
-            LVK_HIP(hipMemset(qkv_gran, 0, 3 * (E / 2) * 8));
-        }
-        if (qkv_attn) {
-            qkv_cnt = (unsigned *) model.alloc(2 * H * QKV_CNT_STRIDE * 4);
-            qkv_cons = qkv_cnt + H * QKV_CNT_STRIDE;
-            LVK_HIP(hipMemset(qkv_cnt, 0, 2 * H * QKV_CNT_STRIDE * 4));
-        }
-        if (attn_beside) {
-            LVK_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-            LVK_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-            LVK_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-        }
+        seq_epochs = L <= 126;
         // test hook (tests/test_gpu_seq_wrap.py): start the step counter near its 25-bit wrap
         if (const char * e = getenv("LVK_SEQ_START")) seq = (unsigned) strtoul(e, nullptr, 0) & ((1u << 25) - 1);
-    }
-    {
-        // persistent decode state: the layer table and the in-launch exchange buffers
-        hipDeviceProp_t prop;
-        int dev_ = 0;
-        LVK_HIP(hipGetDevice(&dev_));
-        LVK_HIP(hipGetDeviceProperties(&prop, dev_));
-        n_cu = prop.multiProcessorCount;
-        std::vector<DecodeLayer> tl(L);
-        for (size_t il = 0; il < L; ++il) {
-            const Layer & ly = model.layers[il];
-            const QMatrix * m4[4] = {&ly.wqkv, &ly.wo, &ly.w13, &ly.w2};
-            for (int k = 0; k < 4; ++k) { tl[il].nib[k] = m4[k]->nib; tl[il].scl[k] = (const float4 *) m4[k]->scl; }
-            tl[il].attn_norm = ly.attn_norm;
-            tl[il].ffn_norm = ly.ffn_norm;
-            tl[il].kc = kc_layer(il);
-            tl[il].vc = vc_layer(il);
-        }
-        dlayers = (DecodeLayer *) model.alloc(std::max<size_t>(1, L) * sizeof(DecodeLayer));
-        if (L) LVK_HIP(hipMemcpy(dlayers, tl.data(), L * sizeof(DecodeLayer), hipMemcpyHostToDevice));
-        const size_t Lx = std::max<size_t>(1, L);
-        xpub = (float *) model.alloc(2 * Lx * E * 4);
-        upub = (float *) model.alloc(Lx * F * 4);
-        qkv_cur = (uint16_t *) model.alloc(Lx * 3 * E * 2);
-        aq_pub_d = (float *) model.alloc(decode_persistent_aq_d_floats((int) E, (int) Lx) * 4);
-        aq_pub_qs = (uint4 *) model.alloc(Lx * (E / 32) * 16);
-        dscratch = model.alloc(decode_persistent_scratch_bytes((int) H, (int) C));
-        // opt-in: measured slower than the launch-per-phase path on 7B
-        const char * ev = getenv("LVK_DECODE_PERSISTENT");
-        decode_persistent = ev && atoi(ev) != 0;
     }
     logits_d = (float *) model.alloc(C * V * 4);
     emb_d = (float *) model.alloc(E * 4);
@@ -232,7 +175,6 @@ void Context::init(const llama_context_params & p) {
     LVK_HIP(hipMemcpy(rope, rt.data(), rt.size() * sizeof(float2), hipMemcpyHostToDevice));
 
     LVK_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-    prepare_persistent();
     logits.reserve(logits_all ? C * V : V);
     if (want_embedding) embedding.resize(E);
 }
@@ -243,7 +185,7 @@ void Context::check_device_error() {
     __atomic_store_n(err_h, 0u, __ATOMIC_RELEASE);
     logits_valid = false;
     throw Error(e == LVK_ERR_ATTN_SPIN ? "llama.vk_amd: decode attention: a workgroup wait timed out (results discarded)"
-                                       : "llama.vk_amd: persistent decode: a phase wait timed out (results discarded)");
+                                       : "llama.vk_amd: a kernel wait timed out (results discarded)");
 }
 
 void Context::timed_launch(int cls, double bytes, const std::function<hipError_t()> & fn) {
@@ -276,45 +218,6 @@ void Context::collect_profile() {
         prof.ms[ev_class[i]] += ms;
     }
     ev_used = 0;
-}
-
-bool Context::persistent_ok() const { return decode_persistent && dargs_d != nullptr; }
-
-// the persistent kernel's arguments never change for a context: built and uploaded once
-void Context::prepare_persistent() {
-    const HParams & hp = model.hp;
-    if (model.layers.empty() || model.qtype != Q4_0 || kv32) return;
-    DecodeArgs A{};
-    A.layers = dlayers;
-    A.n_layer = (int) model.layers.size();
-    A.n_embd = (int) hp.n_embd; A.n_ff = (int) hp.n_ff(); A.n_head = (int) hp.n_head; A.n_ctx = n_ctx;
-    A.n_vocab = (int) hp.n_vocab;
-    if (model.has_head) { A.out_nib = model.output.nib; A.out_scl = (const float4 *) model.output.scl; A.out_norm = model.norm; }
-    A.tok_emb = model.tok_emb;
-    A.emb_type = model.emb_type;
-    A.xin = model.has_embed ? nullptr : x;
-    A.xout = x;
-    A.sp = sp_d;
-    A.logits = logits_d;
-    A.X = xpub; A.U = upub; A.cur = qkv_cur; A.aq_d = aq_pub_d; A.aq_qs = aq_pub_qs;
-    A.exp_tab = exp_tab; A.exp_mode = exp_computed; A.silu_tab = silu_tab; A.rope = rope;
-    A.err = err_d;
-    if (!decode_persistent_prepare(A, dscratch, n_cu)) return;
-    dargs = A;
-    dargs_d = (DecodeArgs *) model.alloc(sizeof(DecodeArgs));
-    LVK_HIP(hipMemcpy(dargs_d, &dargs, sizeof(DecodeArgs), hipMemcpyHostToDevice));
-}
-
-void Context::set_decode_persistent(bool on) {
-    if (on == decode_persistent) return;
-    decode_persistent = on;
-    // the captured decode graphs hold the other path
-    if (graph_exec) { (void) hipGraphExecDestroy(graph_exec); graph_exec = nullptr; }
-    if (graph) { (void) hipGraphDestroy(graph); graph = nullptr; }
-    if (graph_greedy_exec) { (void) hipGraphExecDestroy(graph_greedy_exec); graph_greedy_exec = nullptr; }
-    if (graph_greedy) { (void) hipGraphDestroy(graph_greedy); graph_greedy = nullptr; }
-    if (graph_sample_exec) { (void) hipGraphExecDestroy(graph_sample_exec); graph_sample_exec = nullptr; }
-    if (graph_sample) { (void) hipGraphDestroy(graph_sample); graph_sample = nullptr; }
 }
 
 static double qbytes(const QMatrix & w) { return (double) w.M * (w.K / 32) * (w.qtype == Q4_0 ? 20 : 24); }
@@ -428,25 +331,9 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
             LVK_HIP(launch_rmsnorm_rows(x + (size_t) (n - 1) * E, model.norm, E, 1, emb_d, stream));
         return;
     }
-    if (n == 1 && last_only && head && persistent_ok()) {
-        // the whole token in one launch (decode_persistent.hip)
-        double bytes = model.has_head ? qbytes(model.output) : 0.0;
-        for (const Layer & ly : model.layers) bytes += qbytes(ly.wqkv) + qbytes(ly.wo) + qbytes(ly.w13) + qbytes(ly.w2);
-        timed_launch(K_DECODE, bytes, [&] { return launch_decode_persistent(dargs, dargs_d, n_cu, stream); });
-        if (want_embedding && model.has_head)
-            LVK_HIP(launch_rmsnorm_rows(x, model.norm, E, 1, emb_d, stream));
-        return;
-    }
     // single-token FFN: W1|W3 hands silu(w1 x)*(w3 x) to W2 in f32, W2 quantizes it
     const bool ffn_f32 = n == 1 && matvec_cu_supported(E, model.qtype) && matvec_cu_supported(F, model.qtype);
-    // attention, Wo and the residual add in one launch (attention_decode.hip, k_attn_wo)
-    const bool attn_wo = n == 1 && !old_attention && !kv32 && fuse_attn_wo && model.qtype == Q4_0 && !model.layers.empty() &&
-                         attention_wo_supported(E, H, n_ctx, model.layers[0].wo);
-    const bool seq_ep = seq_epochs && !attn_wo;
-    // (the QKV launch must be the CU-balanced kernel: only its epilogue publishes the granules)
-    const bool beside = attn_beside && n == 1 && !old_attention && !kv32 && seq_ep &&
-                        attention_decode_supported(E, H, n_ctx) && matvec_cu_supported(E, model.qtype);
-    const bool merged = qkv_attn && n == 1 && !old_attention && !kv32 && seq_ep;
+    const bool seq_ep = seq_epochs;
     if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx) && !seq_ep)
         // the decode attention's score granules carry epoch = layer + 1: zero them once per token
         LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes(H, n_ctx), stream));
@@ -466,50 +353,16 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
         at.err = err_d;
         at.kv32 = kv32;
         at.seq_epochs = seq_ep ? 1 : 0;
-        const bool beside_l = beside && !attn_wo;
-        const bool merged_l = merged && !attn_wo;
-        if (merged_l) {
-            a.qkv_gran = qkv_gran;
-            a.qkv_epoch = (unsigned) il + 1;
-        }
-        if (beside_l) {
-            // fork: the attention of this layer on the side stream, from the same point as QKV
-            // (after W2 of the previous layer), joined again before Wo
-            a.qkv_gran = qkv_gran;
-            a.qkv_epoch = (unsigned) il + 1;
-            at.qkv_gran = qkv_gran;
-            at.lds_min = attn_lds_min;
-            LVK_HIP(hipEventRecord(ev_fork, stream));
-            LVK_HIP(hipStreamWaitEvent(side, ev_fork, 0));
-            timed_launch(K_ATTN, 0, [&] { return launch_attention_decode(at, attn_gran, (unsigned) il + 1, side); });
-            LVK_HIP(hipEventRecord(ev_join, side));
-        }
-        if (merged_l)
-            timed_launch(K_QKV, qbytes(ly.wqkv), [&] {
-                return launch_qkv_attn(a, at, attn_gran, (unsigned) il + 1, qkv_cnt, qkv_cons, stream);
-            });
+        timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
+        if (n > 1 && !kv32 && attention_prompt_supported(E, H, n_ctx))
+            timed_launch(K_ATTN, 0, [&] { return launch_attention_prompt(at, (uint16_t *) scores, nullptr, nullptr, stream); });
+        else if (n == 1 && !old_attention && !kv32 && attention_decode_supported(E, H, n_ctx))
+            timed_launch(K_ATTN, 0, [&] { return launch_attention_decode(at, attn_gran, (unsigned) il + 1, stream); });
         else
-            timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
-        if (beside_l) LVK_HIP(hipStreamWaitEvent(stream, ev_join, 0));
-        if (attn_wo) {
-            timed_launch(K_ATTN_WO, qbytes(ly.wo), [&] {
-                return launch_attention_wo(at, ly.wo, x, attn_gran, (unsigned) il + 1, stream);
-            });
-        } else {
-            if (beside_l || merged_l)
-                ;   // launched on the side stream / inside the QKV launch above
-            else if (n > 1 && !kv32 && attention_prompt_supported(E, H, n_ctx))
-                timed_launch(K_ATTN, 0, [&] {
-                    return launch_attention_prompt(at, (uint16_t *) scores, nullptr, nullptr, stream);
-                });
-            else if (n == 1 && !old_attention && !kv32 && attention_decode_supported(E, H, n_ctx))
-                timed_launch(K_ATTN, 0, [&] { return launch_attention_decode(at, attn_gran, (unsigned) il + 1, stream); });
-            else
-                timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
-            MvLaunch b;
-            b.w = ly.wo; b.xq = aq_attn; b.y = x; b.sp = sp_d; b.n_tokens = n;
-            timed_launch(K_WO, qbytes(ly.wo), [&] { return mv_launch(b, PRO_ACTQ, EPI_RESID, stream); });
-        }
+            timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
+        MvLaunch b;
+        b.w = ly.wo; b.xq = aq_attn; b.y = x; b.sp = sp_d; b.n_tokens = n;
+        timed_launch(K_WO, qbytes(ly.wo), [&] { return mv_launch(b, PRO_ACTQ, EPI_RESID, stream); });
         MvLaunch c;
         c.w = ly.w13; c.x = x; c.g = ly.ffn_norm; c.sp = sp_d; c.n_tokens = n; c.silu_tab = silu_tab;
         c.out_q = aq_ffn; c.u = u_ffn;
@@ -589,46 +442,6 @@ int Context::eval_greedy(int token, int n_past) {
     return *greedy_h;
 }
 
-int Context::attn_mode() const { return qkv_attn ? 2 : attn_beside ? 1 : 0; }
-
-// the decode attention beside QKV is safe only if, wherever the dispatcher puts the 4 H
-// attention workgroups, every QKV workgroup can still be placed: the attention requests
-// more than half a CU's LDS (at most one per CU), 4 H <= CUs, and one attention workgroup
-// plus one QKV workgroup fit a CU's LDS, wave slots and each SIMD's 512 registers (footprints
-// of the exact kernels, LVK_LAUNCH's record mode).  Otherwise the attention stays after QKV.
-bool Context::beside_fits() {
-    const HParams & hp = model.hp;
-    const int E = (int) hp.n_embd, H = (int) hp.n_head;
-    KernelFootprint fq, fa;
-    {
-        MvLaunch a;
-        a.w.qtype = model.qtype; a.w.M = 3 * E; a.w.K = E;
-        a.n_tokens = 1; a.n_embd = E; a.head_dim = E / H; a.n_ctx = n_ctx;
-        g_footprint = &fq;
-        const hipError_t e = launch_matvec_cu(a, PRO_NORM, EPI_QKV, nullptr);
-        g_footprint = nullptr;
-        if (e != hipSuccess || !fq.threads) return false;
-    }
-    {
-        static const unsigned long long dummy = 0;
-        AttnLaunch at{};
-        at.out_qtype = model.qtype; at.n_tokens = 1; at.n_embd = E; at.n_head = H; at.n_ctx = n_ctx;
-        at.seq_epochs = 1; at.qkv_gran = &dummy;
-        g_footprint = &fa;
-        const hipError_t e = launch_attention_decode(at, nullptr, 1, nullptr);
-        g_footprint = nullptr;
-        if (e != hipSuccess || !fa.threads) return false;
-    }
-    constexpr size_t LDS_CU = 160 * 1024;
-    const size_t pad = std::max(fa.lds, LDS_CU / 2 + 1024);
-    auto alloc = [](int v) { return (std::max(v, 1) + 7) / 8 * 8; };
-    const int wq = fq.threads / 64, wa = fa.threads / 64;
-    const bool ok = fa.workgroups <= cu_count() && fq.lds + pad <= LDS_CU && wq + wa <= 32 &&
-                    alloc(fq.vgprs) * ((wq + 3) / 4) + alloc(fa.vgprs) * ((wa + 3) / 4) <= 512;
-    if (ok) attn_lds_min = pad;
-    return ok;
-}
-
 // the step counter of the next device step (StepParams::seq); before it would run past the
 // 25 bits that keep (seq << 7) + layer + 1 unique, the granules are zeroed (stream-ordered
 // ahead of the steps that use the restarted counter) and the count restarts
@@ -636,7 +449,6 @@ unsigned Context::next_seq(unsigned k) {
     if (seq + k >= (1u << 25)) {
         if (attn_gran)
             LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes((int) model.hp.n_head, n_ctx), stream));
-        if (qkv_gran) LVK_HIP(hipMemsetAsync(qkv_gran, 0, 3 * (model.hp.n_embd / 2) * 8, stream));
         seq = 0;
     }
     const unsigned first = seq + 1;
@@ -654,7 +466,7 @@ int Context::decode_greedy(int token, int n_past, int n_steps, int * out) {
     if (n_steps <= 0 || n_past < 0 || n_past + n_steps > n_ctx_user)
         throw Error("llama.vk_amd: n_past + n_steps exceeds n_ctx");
     if (token < 0 || token >= (int) model.hp.n_vocab) throw Error("llama.vk_amd: token id out of range");
-    if (!use_graph || profiling || persistent_ok())
+    if (!use_graph || profiling)
         throw Error("llama.vk_amd: greedy decode chains need the launch-per-phase decode graph");
     try {
         StepParams * sh = sp_h;

@@ -19,7 +19,7 @@ struct SplitDel { void operator()(Split * p) const; };
 struct StageLinkDel { void operator()(StageLink * p) const; };
 
 // kernel classes timed by the profiler (events around every launch of a class)
-enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_WO, K_W13, K_W2, K_LMHEAD, K_ATTN_WO, K_DECODE, K_NCLASS };
+enum KClass : int { K_EMBED = 0, K_QKV, K_ATTN, K_WO, K_W13, K_W2, K_LMHEAD, K_NCLASS };
 
 // page-locked host storage: the per-token logits D2H copy runs as one DMA instead of
 // being staged through a driver bounce buffer
@@ -98,25 +98,8 @@ struct Context {
     // prompt (N > 1) path: MFMA matmuls with exact block dots (default) or the
     // bit-faithful VALU kernels (prompt_exact; env LVK_PROMPT_EXACT=1)
     bool prompt_exact = false;
-    bool old_attention = false;
-    // single-token attention + Wo in one launch (k_attn_wo), env LVK_FUSE_ATTN_WO=1: bit-exact but
-    // measured slower than the two launches (17.7 vs 11.5 us per layer at n_past 256), so off
-    bool fuse_attn_wo = false;
-    void * attn_gran = nullptr;  // [H][n_ctx] {tag, score} granules of the decode attention  // env LVK_ATTN_V1=1: single-token evals on the one-kernel attention.hip
-    // decode attention beside QKV (LVK_ATTN_BESIDE): the attention of layer l runs on a second
-    // stream next to QKV(l) and takes the new q / k / v rows as tagged granules
-    bool attn_beside = false;
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    unsigned long long * qkv_gran = nullptr;   // [3][E/2] {tag, f16 pair}
-    size_t attn_lds_min = 0;                   // the attention's LDS request beside QKV
-    bool beside_fits();
-    // QKV and the decode attention in one launch (LVK_QKV_ATTN; matvec_cu.hip k_qkv_attn)
-    bool qkv_attn = false;
-    unsigned * qkv_cnt = nullptr;              // [H] QKV row groups finished per head
-    unsigned * qkv_cons = nullptr;             // [H] attention workgroups that have read them
-    // 0: the decode attention after QKV, 1: beside it on a second stream, 2: merged into it
-    int attn_mode() const;
+    bool old_attention = false;  // env LVK_ATTN_V1=1: single-token evals on the one-kernel attention.hip
+    void * attn_gran = nullptr;  // [H][n_ctx] {tag, score} granules of the decode attention
     uint16_t * xh = nullptr;     // masked MFMA B-fragment image of the quantized activations (mm_act_bytes)
     float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales
     // Q4_0 prompt: the W2 input image written by the W1|W3 epilogue (EPI_SWIGLU_Q; the W1|W3
@@ -128,24 +111,6 @@ struct Context {
     // prompt: RoPE + KV append fused into the QKV matmul (LVK_MM_ROPE=0: separate kernel)
     bool mm_rope_fused = [] { const char * e = getenv("LVK_MM_ROPE"); return !e || atoi(e) != 0; }();
     float * uf = nullptr;        // [C][F] silu(w1 x) * (w3 x)
-
-    // persistent single-token decode (decode_persistent.hip): one launch per token;
-    // opt-in (env LVK_DECODE_PERSISTENT=1 or lvk_set_decode_persistent(ctx, 1)), the
-    // launch-per-phase path is the default
-    bool decode_persistent = false;
-    int n_cu = 0;
-    DecodeLayer * dlayers = nullptr;   // device layer table
-    float * xpub = nullptr;            // [2L][E] published residual stream
-    float * upub = nullptr;            // [L][F] published silu(w1 x) * w3 x
-    uint16_t * qkv_cur = nullptr;      // [L][3E] this token's q | k | v (f16)
-    float * aq_pub_d = nullptr;        // [L][E/32] the quantized attention output
-    uint4 * aq_pub_qs = nullptr;
-    void * dscratch = nullptr;         // counters + score granules (zeroed per launch)
-    DecodeArgs dargs{};                // its launch arguments (prepare_persistent)
-    DecodeArgs * dargs_d = nullptr;    // ... and their device copy (nullptr: shape not supported)
-    bool persistent_ok() const;
-    void prepare_persistent();
-    void set_decode_persistent(bool on);
 
     // decode graph (N = 1, last-token logits)
     hipGraph_t graph = nullptr;
@@ -181,7 +146,7 @@ struct Context {
     int * chain_h = nullptr;     // pinned copy of the tokens
     int decode_greedy(int token, int n_past, int n_steps, int * out);
     // decode attention granule epochs from the step counter (StepParams::seq): no zeroing per
-    // token (off for the fused attention + Wo kernel and models with more than 126 layers)
+    // token (off for models with more than 126 layers)
     bool seq_epochs = false;
     unsigned seq = 0;            // the last step counter handed to the device
     unsigned next_seq(unsigned k = 1);

@@ -319,20 +319,6 @@ size_t lvk_weight_bytes(struct llama_context * ctx) {
 void lvk_set_graph(struct llama_context * ctx, int on) {
     for (lvk::Context * c : ctx->stages()) c->use_graph = on != 0;
 }
-void lvk_set_decode_persistent(struct llama_context * ctx, int on) {
-    for (lvk::Context * c : ctx->stages()) c->set_decode_persistent(on != 0);
-}
-int lvk_attn_mode(struct llama_context * ctx) {
-    int m = -1;
-    for (lvk::Context * c : ctx->stages()) m = m < 0 ? c->attn_mode() : std::min(m, c->attn_mode());
-    return m < 0 ? 0 : m;
-}
-int lvk_decode_persistent_active(struct llama_context * ctx) {
-    for (lvk::Context * c : ctx->stages())
-        if (!c->persistent_ok()) return 0;
-    return 1;
-}
-
 void lvk_set_prompt_exact(struct llama_context * ctx, int on) {
     for (lvk::Context * c : ctx->stages()) c->prompt_exact = on != 0;
 }

@@ -108,10 +108,7 @@ _sig("lvk_get_profile", C.c_int, [C.c_void_p, f64p, i64p, f64p, C.c_int])
 _sig("lvk_reset_profile", None, [C.c_void_p])
 _sig("lvk_weight_bytes", C.c_size_t, [C.c_void_p])
 _sig("lvk_set_graph", None, [C.c_void_p, C.c_int])
-_sig("lvk_set_decode_persistent", None, [C.c_void_p, C.c_int])
-_sig("lvk_decode_persistent_active", C.c_int, [C.c_void_p])
 _sig("lvk_set_prompt_exact", None, [C.c_void_p, C.c_int])
-_sig("lvk_attn_mode", C.c_int, [C.c_void_p])
 _sig("lvk_eval_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_decode_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p])
 _sig("lvk_argmax", C.c_int, [f32p, C.c_int])
@@ -125,13 +122,12 @@ _sig("lvk_stage_layers", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c
 _sig("lvk_rccl_unique_id", C.c_int, [C.c_void_p, C.c_size_t])
 _sig("lvk_stage_connect", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_connect_shm", C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.c_int])
-_sig("lvk_dev_kernels", C.c_int, [])
 _sig("lvk_stage_step", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int])
 _sig("lvk_init_split", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, i32p, C.c_char_p, C.c_int])
 _sig("lvk_split_info", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)])
 
 BLOCK_BYTES = {2: 20, 3: 24}
-KCLASS = ["embed", "qkv", "attention", "wo", "w13", "w2", "lm_head", "attn_wo", "decode"]
+KCLASS = ["embed", "qkv", "attention", "wo", "w13", "w2", "lm_head"]
 
 
 def _check(rc, what):
@@ -294,17 +290,6 @@ class Llama:
 
     def set_graph(self, on):
         lib.lvk_set_graph(self.ctx, int(on))
-
-    def set_decode_persistent(self, on):
-        """single-token evals on the persistent one-launch kernel (True) or one launch per phase (False, default)"""
-        lib.lvk_set_decode_persistent(self.ctx, int(on))
-
-    def decode_persistent_active(self):
-        return bool(lib.lvk_decode_persistent_active(self.ctx))
-
-    def attn_mode(self):
-        """decode attention: 0 after QKV, 1 beside it on a second stream, 2 inside the QKV launch"""
-        return int(lib.lvk_attn_mode(self.ctx))
 
     def set_prompt_exact(self, on):
         """prompt batches on the bit-faithful VALU path (True) or the MFMA path (False, default)"""
@@ -525,11 +510,6 @@ def gen_model(path, n_embd=4096, n_head=32, n_layer=32, ftype=2, seed=1, n_vocab
         cmd += ["--vocab", vocab]
     subprocess.check_call(cmd, stderr=subprocess.DEVNULL)
     return path
-
-
-def dev_kernels():
-    """True when the loaded library is the dev build (parked kernels compiled in)"""
-    return bool(lib.lvk_dev_kernels())
 
 
 def rccl_unique_id():

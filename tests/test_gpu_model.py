@@ -131,36 +131,6 @@ def test_7b_shaped_decode_vs_oracle(lvk, oracle, model_dir, n_prompt):
     om.close()
 
 
-def test_7b_shaped_fused_attention_wo_matches(lvk, oracle, model_dir, monkeypatch):
-    """The opt-in one-launch attention + Wo (k_attn_wo, LVK_FUSE_ATTN_WO=1) on LLaMA-7B
-    layer shapes: decode logits bit-identical to the oracle across 40 positions."""
-    from oracle_lib import gen_model
-    if not lvk.dev_kernels():
-        pytest.skip("parked kernel: run with LVK_LIB=llama.vk_amd/lib/dev/libllama_vk_amd.so")
-    path = gen_model(os.path.join(model_dir, "w4096_l2.bin"), n_embd=4096, n_head=32, n_layer=2, ftype=2, seed=7)
-    monkeypatch.setenv("LVK_FUSE_ATTN_WO", "1")
-    m = lvk.Llama(path, n_ctx=512)
-    om = oracle.model(path, 512)
-    toks = np.array([1, 450, 4996, 17354, 1701, 29916, 338, 263], np.int32)
-    a = m.eval(toks, 0)
-    b = om.eval(toks, 0)
-    assert np.array_equal(bits(a), bits(b))
-    n_past, tok = len(toks), int(np.argmax(a[-1]))
-    for _ in range(40):
-        a = m.eval([tok], n_past)
-        b = om.eval([tok], n_past)
-        assert np.array_equal(bits(a), bits(b)), "n_past %d" % n_past
-        n_past += 1
-        tok = int(np.argmax(a[-1]))
-    m.set_profiling(True)
-    m.eval([tok], n_past)
-    assert m.profile()["attn_wo"]["launches"] == 2      # the fused kernel ran (one per layer)
-    m.close()
-    om.close()
-
-
-@pytest.mark.parametrize("cfg,steps", [(dict(n_embd=5120, n_head=40, n_layer=2, seed=11), 12),
-                                       (dict(n_embd=4096, n_head=32, n_layer=2, seed=12), 8)])
 def test_q4_1_shaped_decode_vs_oracle(lvk, oracle, model_dir, cfg, steps):
     """LLaMA-13B (n_embd 5120, n_ff 13824, 40 heads) and 7B layer shapes in Q4_1, 2 layers:
     Q4_1 quantizer, the CU-balanced Q4_1 decode matvecs (matvec_cu41.hip: QKV + RoPE, Wo,

@@ -134,10 +134,8 @@ int main(int argc, char ** argv) {
             AttnLaunch at{q16, kc + (size_t) l * C * E, vc + (size_t) l * C * E, scores, aqa, Q4_0, etab, sp, 1, E, H, C};
             at.exp_computed = exp_mode;   // timing only: random table, mode of the real table check
             if (getenv("LVK_ATTN_V1")) CK(launch_attention(at, s));
-            else if (getenv("LVK_PROBE_FUSE")) CK(launch_attention_wo(at, y.wo, x, gran, (unsigned) l + 1, s));
             else CK(launch_attention_decode(at, gran, (unsigned) l + 1, s));
         } else if (k == 2) {
-            if (getenv("LVK_PROBE_FUSE")) return;   // inside the attention launch (k_attn_wo)
             MvLaunch b; b.w = y.wo; b.xq = aqa; b.y = x; b.sp = sp; b.n_tokens = 1;
             CK(mv(b, PRO_ACTQ, EPI_RESID));
         } else if (k == 3) {
