@@ -111,14 +111,24 @@ LVK_API void lvk_set_graph(struct llama_context * ctx, int on);
  * lvk_argmax(x, n) is the op-level kernel on a host array: the first index whose
  * value is strictly greater than all earlier ones (0 when x[0] is NaN). */
 LVK_API int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past);
-/* n_steps greedy decode steps in one call: out_tokens[i] is what the i-th of the calls
- * t = lvk_eval_greedy(ctx, t, n_past + i) (t starting at `token`) would return, and the KV
- * cache ends in the same state.  The steps run as back-to-back replays of one decode graph
- * whose last kernel advances the step block and writes the next embedding row on the device,
- * so nothing crosses PCIe between steps.  n_past + n_steps <= n_ctx.  Returns 0, or -1 on
- * error (layer splits and logits_all contexts refuse it).
- * The host logits of llama_get_logits are NOT refreshed. */
+/* n_steps decode steps in one call: step i evaluates token t_i at position n_past + i, with
+ * t_0 = tokens[0], t_{i+1} = tokens[i + 1] while i + 1 < n_tokens (a teacher-forced sequence,
+ * 1 <= n_tokens <= n_steps) and the argmax of step i's logits after that (n_tokens = 1: greedy).
+ * out_tokens[i] is the argmax of step i's logits (what lvk_eval_greedy(ctx, t_i, n_past + i)
+ * returns); out_digests (optional, may be NULL) receives lvk_logits_digest of step i's logits
+ * row, computed on the device, so a caller can check every step's logits without copying them.
+ * The KV cache ends as after the n_steps single-token evals.  The steps run as back-to-back
+ * replays of one decode graph whose last kernel picks the next token, advances the step block and
+ * writes the next embedding row on the device, so nothing crosses PCIe between steps.
+ * n_past + n_steps <= n_ctx.  Returns 0, or -1 on error (layer splits and logits_all contexts
+ * refuse it).  The host logits of llama_get_logits are NOT refreshed. */
+LVK_API int lvk_decode_chain(struct llama_context * ctx, const int * tokens, int n_tokens, int n_past, int n_steps,
+                             int * out_tokens, uint64_t * out_digests);
+/* lvk_decode_chain(ctx, &token, 1, n_past, n_steps, out_tokens, NULL) */
 LVK_API int lvk_decode_greedy(struct llama_context * ctx, int token, int n_past, int n_steps, int * out_tokens);
+/* digest of a logits row: sum over k (mod 2^64) of splitmix64((k << 32) | bits(x[k])) -- position
+ * sensitive, order independent, equal for two rows only if (almost surely) bit-identical */
+LVK_API uint64_t lvk_logits_digest(const float * x, int n);
 /* On-device sampling: lvk_eval_sample(ctx, token, n_past, last_n, n_last,
  * top_k, top_p, temp, repeat_penalty) returns what llama_eval(ctx, &token, 1, n_past, .)
  * followed by llama_sample_top_p_top_k(ctx, last_n, n_last, top_k, top_p, temp,

@@ -291,11 +291,14 @@ hipError_t launch_rmsnorm_rows(const float * x, const float * g, int K, int n, f
 // greedy argmax over x[0..n) with the reference's first-maximum rule (llama.cpp:1382-1394); *out on the device
 // (out2, optional: a second copy of the token, e.g. host-mapped memory)
 hipError_t launch_argmax(const float * x, int n, int * out, hipStream_t s, int * out2 = nullptr);
-// one chained greedy step's tail (lvk_decode_greedy): the same argmax, the token into
-// chain[1 + chain[0]++], the step block advanced (n_past + 1, token, seq + 1) and the token's
-// embedding row (launch_embed's) into x[0..n_embd)
-hipError_t launch_argmax_step(const float * logits, int n, StepParams * sp, int * chain, const void * emb, int emb_type,
-                              int n_embd, float * x, hipStream_t s);
+// one chained decode step's tail (lvk_decode_chain): the same argmax into chain[CHAIN_HDR + i]
+// (chain[0] = i counts the steps), the logits digest into digest[i] when chain[2] != 0, the next
+// token (forced[i + 1] while i + 1 < chain[1], else the argmax) into the step block (n_past + 1,
+// token, seq + 1) and its embedding row (launch_embed's) into x[0..n_embd)
+constexpr int CHAIN_HDR = 4;
+hipError_t launch_argmax_step(const float * logits, int n, StepParams * sp, int * chain, const int * forced,
+                              unsigned long long * digest, const void * emb, int emb_type, int n_embd, float * x,
+                              hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // ggml graph operators (graph_ops.hip; include/ggml.h via runtime/ggml_graph.cpp): one

@@ -372,15 +372,28 @@ __global__ __launch_bounds__(1024) void k_argmax_first(const float * __restrict_
     }
 }
 
-// the last kernel of a chained greedy step (lvk_decode_greedy): the argmax of k_argmax_first
-// is the next token; it goes to chain[1 + i] (chain[0] counts the steps), into the step block
-// (n_past + 1, the token, seq + 1) and, as its embedding row (k_embed's dequantization), into
-// x -- everything the next replay of the step graph reads
+// the last kernel of a chained decode step (lvk_decode_chain): the argmax of k_argmax_first
+// goes to chain[CHAIN_HDR + i] (chain[0] counts the steps), the digest of the logits row
+// (lvk_logits_digest) to digest[i] when chain[2] != 0, and the next token -- forced[i + 1] while
+// i + 1 < chain[1] (a teacher-forced sequence), else the argmax -- into the step block (n_past + 1,
+// the token, seq + 1) and, as its embedding row (k_embed's dequantization), into x: everything
+// the next replay of the step graph reads
+__device__ __forceinline__ unsigned long long digest_mix(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;                      // splitmix64 finalizer
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
 __global__ __launch_bounds__(1024) void k_argmax_step(const float * __restrict__ logits, int n, StepParams * sp,
-                                                      int * chain, const uint8_t * __restrict__ emb, int type, int E,
+                                                      int * chain, const int * __restrict__ forced,
+                                                      unsigned long long * __restrict__ digest,
+                                                      const uint8_t * __restrict__ emb, int type, int E,
                                                       float * __restrict__ x) {
     __shared__ ArgBest red[16];
+    __shared__ unsigned long long dred[16];
     __shared__ int s_tok;
+    const int i = chain[0], n_forced = chain[1];
+    const bool want_digest = chain[2] != 0;
     ArgBest b = arg_scan(logits, n);
     for (int off = 32; off > 0; off >>= 1) {
         ArgBest o;
@@ -389,16 +402,29 @@ __global__ __launch_bounds__(1024) void k_argmax_step(const float * __restrict__
         b = arg_pick(b, o);
     }
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    if (want_digest) {
+        // sum over the row of mix(index << 32 | bits): wrap-around adds, any order gives the same
+        unsigned long long dg = 0;
+        for (int k = threadIdx.x; k < n; k += 1024)
+            dg += digest_mix(((unsigned long long) k << 32) | __float_as_uint(logits[k]));
+        for (int off = 32; off > 0; off >>= 1) dg += __shfl_xor(dg, off, 64);
+        if ((threadIdx.x & 63) == 0) dred[threadIdx.x >> 6] = dg;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         ArgBest r = red[0];
         for (int w = 1; w < 16; ++w) r = arg_pick(r, red[w]);
         const bool nan0 = n > 0 && !(logits[0] == logits[0]);
-        const int tok = (nan0 || r.i == INT_MAX) ? 0 : r.i;
+        const int amax = (nan0 || r.i == INT_MAX) ? 0 : r.i;
+        const int tok = i + 1 < n_forced ? forced[i + 1] : amax;
         s_tok = tok;
-        const int i = chain[0];
-        chain[1 + i] = tok;
+        chain[CHAIN_HDR + i] = amax;
         chain[0] = i + 1;
+        if (want_digest) {
+            unsigned long long dg = 0;
+            for (int w = 0; w < 16; ++w) dg += dred[w];
+            digest[i] = dg;
+        }
         StepParams st = *sp;
         st.n_past += 1;
         st.pad0 = tok;
@@ -432,10 +458,12 @@ __global__ __launch_bounds__(1024) void k_argmax_step(const float * __restrict__
 }
 }  // namespace
 
-hipError_t launch_argmax_step(const float * logits, int n, StepParams * sp, int * chain, const void * emb, int emb_type,
-                              int n_embd, float * x, hipStream_t s) {
+hipError_t launch_argmax_step(const float * logits, int n, StepParams * sp, int * chain, const int * forced,
+                              unsigned long long * digest, const void * emb, int emb_type, int n_embd, float * x,
+                              hipStream_t s) {
     if (n <= 0 || n_embd <= 0 || n_embd % 32) return hipErrorInvalidValue;
-    LVK_LAUNCH(k_argmax_step, dim3(1), dim3(1024), 0, s, logits, n, sp, chain, (const uint8_t *) emb, emb_type, n_embd, x);
+    LVK_LAUNCH(k_argmax_step, dim3(1), dim3(1024), 0, s, logits, n, sp, chain, forced, digest, (const uint8_t *) emb,
+               emb_type, n_embd, x);
     return hipGetLastError();
 }
 

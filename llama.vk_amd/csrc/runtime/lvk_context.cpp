@@ -69,6 +69,9 @@ Context::~Context() {
     if (graph_chain_exec) (void) hipGraphExecDestroy(graph_chain_exec);
     if (graph_chain) (void) hipGraphDestroy(graph_chain);
     if (chain_h) (void) hipHostFree(chain_h);
+    if (chain_ctl_h) (void) hipHostFree(chain_ctl_h);
+    if (forced_h) (void) hipHostFree(forced_h);
+    if (digest_h) (void) hipHostFree(digest_h);
     if (samp_h) (void) hipHostFree(samp_h);
     if (sout_h) (void) hipHostFree(sout_h);
     if (greedy_h) (void) hipHostFree(greedy_h);
@@ -144,8 +147,13 @@ void Context::init(const llama_context_params & p) {
     *err_h = 0;
     LVK_HIP(hipHostGetDevicePointer((void **) &err_d, err_h, 0));
     greedy_d = (int *) model.alloc(4);
-    chain_d = (int *) model.alloc((1 + C) * 4);
+    chain_d = (int *) model.alloc((CHAIN_HDR + C) * 4);
+    forced_d = (int *) model.alloc(C * 4);
+    digest_d = (unsigned long long *) model.alloc(C * 8);
     LVK_HIP(hipHostMalloc((void **) &chain_h, C * 4, hipHostMallocDefault));
+    LVK_HIP(hipHostMalloc((void **) &chain_ctl_h, CHAIN_HDR * 4, hipHostMallocDefault));
+    LVK_HIP(hipHostMalloc((void **) &forced_h, C * 4, hipHostMallocDefault));
+    LVK_HIP(hipHostMalloc((void **) &digest_h, C * 8, hipHostMallocDefault));
     // the device argmax also stores the token straight into host-mapped memory
     LVK_HIP(hipHostMalloc((void **) &greedy_h, 64, hipHostMallocMapped | hipHostMallocCoherent));
     LVK_HIP(hipHostGetDevicePointer((void **) &greedy_hd, greedy_h, 0));
@@ -397,7 +405,7 @@ void Context::build_graph(int kind) {
             // a chained step: the step block and x were left by the previous step (or the
             // call's setup); the argmax advances both for the next replay
             enqueue_forward(1, true, nullptr, 0, true, false);
-            LVK_HIP(launch_argmax_step(logits_d, (int) model.hp.n_vocab, sp_d, chain_d, model.tok_emb, model.emb_type,
+            LVK_HIP(launch_argmax_step(logits_d, (int) model.hp.n_vocab, sp_d, chain_d, forced_d, digest_d, model.tok_emb, model.emb_type,
                                        (int) model.hp.n_embd, x, stream));
         } else {
             LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
@@ -456,30 +464,45 @@ unsigned Context::next_seq(unsigned k) {
     return first;
 }
 
-// n_steps greedy decode steps in one call (lvk_decode_greedy): the same tokens as n_steps
-// calls of eval_greedy(token_i, n_past + i) with token_{i+1} their result, but the host
-// only sets the step block up once and replays the chained graph back to back (no host
-// round trip, step-block copy or embedding launch between the steps).  out[0..n_steps).
-int Context::decode_greedy(int token, int n_past, int n_steps, int * out) {
-    if (!model.has_head || !model.has_embed) throw Error("llama.vk_amd: greedy decode needs the whole model");
-    if (logits_all) throw Error("llama.vk_amd: greedy decode needs last-token logits");
+// n_steps decode steps in one call (lvk_decode_chain): step i evaluates token t_i at n_past + i,
+// t_0 = tokens[0], t_{i+1} = tokens[i + 1] while i + 1 < n_tokens (teacher forcing), else the
+// argmax of step i's logits (greedy: n_tokens = 1).  The same logits as n_steps single-token
+// evals, but the host only sets the step block up once and replays the chained graph back to back
+// (no host round trip, step-block copy or embedding launch between the steps).  out[i]: the
+// argmax of step i; digests (optional): lvk_logits_digest of step i's logits row.
+int Context::decode_chain(const int * tokens, int n_tokens, int n_past, int n_steps, int * out,
+                          unsigned long long * digests) {
+    if (!model.has_head || !model.has_embed) throw Error("llama.vk_amd: chained decode needs the whole model");
+    if (logits_all) throw Error("llama.vk_amd: chained decode needs last-token logits");
     if (n_steps <= 0 || n_past < 0 || n_past + n_steps > n_ctx_user)
         throw Error("llama.vk_amd: n_past + n_steps exceeds n_ctx");
-    if (token < 0 || token >= (int) model.hp.n_vocab) throw Error("llama.vk_amd: token id out of range");
+    if (!tokens || n_tokens < 1 || n_tokens > n_steps) throw Error("llama.vk_amd: chained decode needs 1..n_steps tokens");
+    for (int i = 0; i < n_tokens; ++i)
+        if (tokens[i] < 0 || tokens[i] >= (int) model.hp.n_vocab) throw Error("llama.vk_amd: token id out of range");
     if (!use_graph || profiling)
-        throw Error("llama.vk_amd: greedy decode chains need the launch-per-phase decode graph");
+        throw Error("llama.vk_amd: chained decode needs the launch-per-phase decode graph");
     try {
         StepParams * sh = sp_h;
         sh->n_past = n_past;
         sh->n_tokens = 1;
-        sh->pad0 = token;
+        sh->pad0 = tokens[0];
         sh->seq = next_seq((unsigned) n_steps);     // the steps take seq, seq + 1, ...
         LVK_HIP(hipMemcpyAsync(sp_d, sh, sizeof(StepParams), hipMemcpyHostToDevice, stream));
-        LVK_HIP(hipMemsetAsync(chain_d, 0, sizeof(int), stream));
+        chain_ctl_h[0] = 0;
+        chain_ctl_h[1] = n_tokens > 1 ? n_tokens : 0;
+        chain_ctl_h[2] = digests ? 1 : 0;
+        chain_ctl_h[3] = 0;
+        LVK_HIP(hipMemcpyAsync(chain_d, chain_ctl_h, CHAIN_HDR * 4, hipMemcpyHostToDevice, stream));
+        if (n_tokens > 1) {
+            std::memcpy(forced_h, tokens, sizeof(int) * (size_t) n_tokens);
+            LVK_HIP(hipMemcpyAsync(forced_d, forced_h, sizeof(int) * (size_t) n_tokens, hipMemcpyHostToDevice, stream));
+        }
         LVK_HIP(launch_embed(model.tok_emb, model.emb_type, (int) model.hp.n_embd, &sp_d->pad0, 1, x, stream));
         if (!graph_chain_exec) build_graph(3);
         for (int i = 0; i < n_steps; ++i) LVK_HIP(hipGraphLaunch(graph_chain_exec, stream));
-        LVK_HIP(hipMemcpyAsync(chain_h, chain_d + 1, sizeof(int) * (size_t) n_steps, hipMemcpyDeviceToHost, stream));
+        LVK_HIP(hipMemcpyAsync(chain_h, chain_d + CHAIN_HDR, sizeof(int) * (size_t) n_steps, hipMemcpyDeviceToHost, stream));
+        if (digests)
+            LVK_HIP(hipMemcpyAsync(digest_h, digest_d, 8 * (size_t) n_steps, hipMemcpyDeviceToHost, stream));
     } catch (...) {
         (void) hipStreamSynchronize(stream);
         logits_valid = false;
@@ -487,6 +510,7 @@ int Context::decode_greedy(int token, int n_past, int n_steps, int * out) {
     }
     end_eval(true);
     std::memcpy(out, chain_h, sizeof(int) * (size_t) n_steps);
+    if (digests) std::memcpy(digests, digest_h, 8 * (size_t) n_steps);
     return out[n_steps - 1];
 }
 

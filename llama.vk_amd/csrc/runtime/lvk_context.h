@@ -142,9 +142,14 @@ struct Context {
     // on the device and writes the next step's embedding row -- replayed n times per call
     hipGraph_t graph_chain = nullptr;
     hipGraphExec_t graph_chain_exec = nullptr;
-    int * chain_d = nullptr;     // [1 + n_ctx]: step counter, then the tokens
+    int * chain_d = nullptr;     // [CHAIN_HDR + n_ctx]: step counter, forced count, digest flag, pad; the argmax tokens
     int * chain_h = nullptr;     // pinned copy of the tokens
-    int decode_greedy(int token, int n_past, int n_steps, int * out);
+    int * chain_ctl_h = nullptr; // pinned header block (CHAIN_HDR ints)
+    int * forced_d = nullptr;    // [n_ctx] teacher-forced tokens of a chained decode
+    int * forced_h = nullptr;    // pinned staging of them
+    unsigned long long * digest_d = nullptr;   // [n_ctx] per-step logits digests
+    unsigned long long * digest_h = nullptr;   // pinned copy
+    int decode_chain(const int * tokens, int n_tokens, int n_past, int n_steps, int * out, unsigned long long * digests);
     // decode attention granule epochs from the step counter (StepParams::seq): no zeroing per
     // token (off for models with more than 126 layers)
     bool seq_epochs = false;

@@ -393,8 +393,9 @@ int lvk_eval_greedy(struct llama_context * ctx, int token, int n_past) {
     return r;
 }
 
-int lvk_decode_greedy(struct llama_context * ctx, int token, int n_past, int n_steps, int * out_tokens) {
-    if (!ctx || !out_tokens) {
+int lvk_decode_chain(struct llama_context * ctx, const int * tokens, int n_tokens, int n_past, int n_steps,
+                     int * out_tokens, uint64_t * out_digests) {
+    if (!ctx || !tokens || !out_tokens) {
         fprintf(stderr, "%s: null argument\n", __func__);
         return -1;
     }
@@ -405,7 +406,7 @@ int lvk_decode_greedy(struct llama_context * ctx, int token, int n_past, int n_s
     lvk::Context & c = ctx->c;
     const int64_t t0 = lvk::now_us();
     try {
-        c.decode_greedy(token, n_past, n_steps, out_tokens);
+        c.decode_chain(tokens, n_tokens, n_past, n_steps, out_tokens, (unsigned long long *) out_digests);
     } catch (const lvk::Error & e) {
         fprintf(stderr, "%s: failed to eval: %s\n", __func__, e.msg.c_str());
         return -1;
@@ -413,6 +414,23 @@ int lvk_decode_greedy(struct llama_context * ctx, int token, int n_past, int n_s
     c.t_eval_us += lvk::now_us() - t0;   // n_steps decode evals (llama.cpp:1186-1195)
     c.n_eval += n_steps;
     return 0;
+}
+
+int lvk_decode_greedy(struct llama_context * ctx, int token, int n_past, int n_steps, int * out_tokens) {
+    return lvk_decode_chain(ctx, &token, 1, n_past, n_steps, out_tokens, nullptr);
+}
+
+uint64_t lvk_logits_digest(const float * x, int n) {
+    uint64_t d = 0;
+    for (int k = 0; k < n; ++k) {
+        uint32_t bits;
+        std::memcpy(&bits, x + k, 4);
+        uint64_t z = ((uint64_t) k << 32 | bits) + 0x9E3779B97F4A7C15ull;   // splitmix64 finalizer
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        d += z ^ (z >> 31);
+    }
+    return d;
 }
 
 }  // extern "C"

@@ -111,6 +111,8 @@ _sig("lvk_set_graph", None, [C.c_void_p, C.c_int])
 _sig("lvk_set_prompt_exact", None, [C.c_void_p, C.c_int])
 _sig("lvk_eval_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_decode_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p])
+_sig("lvk_decode_chain", C.c_int, [C.c_void_p, i32p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p])
+_sig("lvk_logits_digest", C.c_uint64, [f32p, C.c_int])
 _sig("lvk_argmax", C.c_int, [f32p, C.c_int])
 _sig("lvk_sample_candidates", C.c_int, [f32p, C.c_int, i32p, C.c_int, C.c_int, C.c_float, C.c_float, f32p, i32p, C.POINTER(C.c_int)])
 _sig("lvk_kv_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_int])
@@ -127,6 +129,18 @@ _sig("lvk_init_split", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, i
 _sig("lvk_split_info", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)])
 
 BLOCK_BYTES = {2: 20, 3: 24}
+
+
+def logits_digest(row):
+    """lvk_logits_digest in numpy: sum (mod 2^64) over k of splitmix64((k << 32) | bits(row[k]))"""
+    bits = np.ascontiguousarray(row, np.float32).view(np.uint32).astype(np.uint64)
+    z = (np.arange(bits.size, dtype=np.uint64) << np.uint64(32)) | bits
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+        return int(np.sum(z, dtype=np.uint64))
 KCLASS = ["embed", "qkv", "attention", "wo", "w13", "w2", "lm_head"]
 
 
@@ -197,6 +211,21 @@ class Llama:
         if r != 0:
             raise RuntimeError("lvk_decode_greedy failed")
         return out
+
+    def decode_chain(self, tokens, n_past, n_steps=None, digests=True):
+        """n_steps chained decode steps in one call (lvk_decode_chain): step i evaluates tokens[i]
+        (teacher forcing) while i < len(tokens), then the previous step's argmax.  Returns the
+        per-step argmax tokens (int32) and, with digests=True, the per-step logits digests
+        (uint64, logits_digest of each step's logits row, computed on the device)."""
+        t = np.ascontiguousarray(tokens, np.int32).reshape(-1)
+        n_steps = len(t) if n_steps is None else int(n_steps)
+        out = np.zeros(n_steps, np.int32)
+        dg = np.zeros(n_steps, np.uint64) if digests else None
+        r = lib.lvk_decode_chain(self.ctx, t, len(t), int(n_past), n_steps, out.ctypes.data,
+                                 dg.ctypes.data if digests else None)
+        if r != 0:
+            raise RuntimeError("lvk_decode_chain failed")
+        return (out, dg) if digests else out
 
     # ---- pipeline stage (lvk_init_stage contexts)
     def stage_eval(self, tokens, n_tokens, n_past):

@@ -201,3 +201,10 @@ def gen_model(path, n_embd=256, n_head=2, n_layer=32, ftype=2, seed=1, n_vocab=3
 def prompt_tokens(n, start=1):
     """SURVEY.md C3 prompt: [1] + [100 + (i*7919) % 31000 ...]"""
     return np.array([start] + [100 + (i * 7919) % 31000 for i in range(1, n)], np.int32)
+
+
+def forced_tokens(n, seed=5):
+    """a seeded, non-repeating teacher-forced token sequence (ids 3..31999): decode steps fed these
+    read a KV cache whose rows all differ, unlike the greedy stream of a synthetic model, which
+    settles on one token"""
+    return np.random.RandomState(seed).permutation(np.arange(3, 32000, dtype=np.int32))[:n].astype(np.int32)

@@ -5,7 +5,10 @@ measures -- on ONE GPU through the library, compared with the REFERENCE build
 path compiled from the reference sources) on the same tokens and the same batch chunking:
 
   * a 16-token prompt batch (the Q4_0 MFMA prompt path at K = 8192 / 22016) then 3 greedy
-    decode steps (the decode kernels compiled for the 65B row lengths, the 64-head attention).
+    decode steps (the decode kernels compiled for the 65B row lengths, the 64-head attention);
+  * 136 teacher-forced decode steps (n_past 16..151: the 64-head decode attention through its
+    no-exchange path and, past n_kv 128, the score exchange), every step's logits bit-identical
+    to the reference build and lvk_decode_chain's per-step digests equal to the reference's.
 
 The bar is bit-identical logits, as for the full 7B (tests/test_gpu_7b_full.py).
 """
@@ -57,3 +60,8 @@ def test_65b_full_prompt16_decode_vs_reference(model65b, ref):
     m.close()
     rm.close()
 
+
+
+def test_65b_full_context_decode_to_151_vs_reference(model65b, ref):
+    from test_gpu_7b_full import _full_context
+    _full_context(model65b, ref, 151, greedy_steps=4)

@@ -72,39 +72,52 @@ def test_7b_full_prompt512_vs_reference(model7b, ref):
     rm.close()
 
 
-def _full_context(model, ref, last, check_chained=True):
-    """16-token prompt, then greedy decode at n_past 16..last on the GPU library and on the
-    reference build, both fed the reference's greedy token: the logits must be bit-identical
-    at every step (every n_kv the decode attention sees: its no-exchange path up to n_kv 128
-    and the score-exchange path beyond, ggml.c:1781-1815,7062-7130, llama.cpp:1010-1061), and
-    lvk_decode_greedy's chained token stream over the same positions must equal the
-    reference's."""
+def _full_context(model, ref, last, check_chained=True, greedy_steps=16):
+    """16-token prompt, then decode at n_past 16..last on the GPU library and on the reference
+    build, both teacher-forced with the same seeded non-repeating tokens (oracle_lib.forced_tokens:
+    every KV row differs, unlike a synthetic model's greedy stream): the logits must be
+    bit-identical at every step (every n_kv the decode attention sees: its no-exchange path up to
+    n_kv 128 and the score-exchange path beyond, ggml.c:1781-1815,7062-7130,
+    llama.cpp:1010-1061).  Then lvk_decode_chain replays the same forced sequence on the device:
+    its per-step logits digests must equal those of the reference's rows and its per-step argmax
+    the reference's.  Last, greedy_steps of the chained greedy stream against the reference's."""
     import lvk
-    from oracle_lib import prompt_tokens
+    from oracle_lib import forced_tokens, prompt_tokens
     m = lvk.Llama(model, n_ctx=512)
     rm = ref.model(model, 512)
     toks = prompt_tokens(16)
     m.eval(toks, 0)
     b = rm.eval(toks, 0, n_threads=_threads())
-    tok0 = tok = int(np.argmax(b[-1]))
-    stream, bad = [], []
-    for n_past in range(16, last + 1):
-        a = m.eval([tok], n_past)
-        b = rm.eval([tok], n_past, n_threads=_threads())
+    tok0 = int(np.argmax(b[-1]))
+    seq = forced_tokens(last + 1 - 16)
+    bad, digests, amax = [], [], []
+    for i, n_past in enumerate(range(16, last + 1)):
+        a = m.eval([int(seq[i])], n_past)
+        b = rm.eval([int(seq[i])], n_past, n_threads=_threads())
         if not np.array_equal(bits(a[-1]), bits(b[-1])):
             bad.append(n_past)
-        tok = int(np.argmax(b[-1]))
-        stream.append(tok)
+        digests.append(lvk.logits_digest(b[-1]))
+        amax.append(int(np.argmax(b[-1])))
     assert not bad, "decode logits differ at n_past %s" % bad[:20]
     if check_chained:
         m.eval(toks, 0)
-        got = [int(t) for t in m.decode_greedy(tok0, 16, last + 1 - 16)]
-        assert got == stream, "chained greedy tokens differ from the reference from step %d" % next(
-            i for i, (x, y) in enumerate(zip(got, stream)) if x != y)
+        got, dg = m.decode_chain(seq, 16)
+        diff = [16 + i for i, (x, y) in enumerate(zip(dg.tolist(), digests)) if x != y]
+        assert not diff, "chained (teacher-forced) logits digests differ at n_past %s" % diff[:20]
+        assert got.tolist() == amax, "chained argmax differs from the reference's"
+        # the greedy chain from the prompt (degenerate on synthetic weights: kept short)
+        m.eval(toks, 0)
+        rm.eval(toks, 0, n_threads=_threads())
+        want, tok = [], tok0
+        for i in range(greedy_steps):
+            tok = int(np.argmax(rm.eval([tok], 16 + i, n_threads=_threads())[-1]))
+            want.append(tok)
+        assert [int(t) for t in m.decode_greedy(tok0, 16, greedy_steps)] == want
     m.close()
     rm.close()
 
 
 def test_7b_full_context_decode_to_511_vs_reference(model7b, ref):
-    """BASELINE configs[1] over the whole n_ctx 512 window: 496 decode steps (n_past 16..511)"""
+    """BASELINE configs[1] over the whole n_ctx 512 window: 496 teacher-forced decode steps
+    (n_past 16..511)"""
     _full_context(model7b, ref, 511)
