@@ -4,9 +4,12 @@
 A step = one llama_eval of one token (the reference main's greedy loop:
 llama_eval -> argmax of the returned logits -> next token), on a seeded
 synthetic 7B Q4_0 ggjt file (no checkpoints exist here).  Workload: 16-token
-prompt, then greedy decode over positions 16..511 of an n_ctx=512 context
-(positions wrap when --steps exceeds 496).  Weights and KV cache are resident
-in HBM before the timed region.
+prompt, the context window filled once (positions 16..511, untimed), then K
+timed greedy decode steps at positions spread evenly over 16..511 of the n_ctx
+512 window (K = 496: every position in order; K > 496 wraps), so the rate is
+the whole window's average whatever K is (the decode attention's cost grows
+with the position).  Weights and KV cache are resident in HBM before the timed
+region.
 
 Also reported on the same line:
   prompt_eval   one 512-token llama_eval (BASELINE.json configs[2]), best of 3
@@ -320,6 +323,7 @@ def cpu_baseline(path, budget_s=20.0, label="7B Q4_0", prompt=True, seg_steps=16
 
 SPLIT_TIMEOUT_S = 420
 SPLIT_FIRST_TOKEN = 1000       # the greedy token the split's first decode step embeds
+SPLIT_FORCED_STEPS = 16        # teacher-forced steps whose logits digests the split must reproduce
 
 
 def split_child(args):
@@ -371,10 +375,21 @@ def split_child(args):
             st.stage_step(p512 if first else None, 512, 0, micro=micro)
             best = min(best, time.perf_counter() - t0)
         pre[micro] = best
+    # teacher-forced check pass: the 16-token prompt again, then SPLIT_FORCED_STEPS seeded
+    # non-repeating tokens one step at a time (no greedy relay); the last stage digests every
+    # step's logits row (lvk_logits_digest), compared with one unsplit context by rank 0
+    from oracle_lib import forced_tokens
+    st.stage_step(ptoks if first else None, 16, 0, micro=args.split_micro)
+    fdig = []
+    for i, t in enumerate(forced_tokens(SPLIT_FORCED_STEPS)):
+        st.stage_step(np.array([t], np.int32) if first else None, 1, 16 + i)
+        if s == S - 1:
+            fdig.append(lvk.logits_digest(st.logits()[-1]))
     st.close()
     print(json.dumps({"stage": s, "layers": list(lr), "load_s": load_s, "decode_s": dec,
                       "prefill_s": pre[args.split_micro], "prefill_nomicro_s": pre[0],
-                      "tokens": toks if first else None, "prompt_logits_digest": lhash}), flush=True)
+                      "tokens": toks if first else None, "prompt_logits_digest": lhash,
+                      "forced_digests": [str(d) for d in fdig] if s == S - 1 else None}), flush=True)
 
 
 def logits_digest(row):
@@ -384,19 +399,24 @@ def logits_digest(row):
 
 
 def greedy_tokens_1gpu(path, n):
-    """the same greedy steps as a split's stages (16-token prompt, then SPLIT_FIRST_TOKEN at
-    n_past 16, ...) on one unsplit context: what the split's token stream must equal; also
-    the digest of the prompt's last logits row"""
+    """the same steps as a split's stages on one unsplit context: the greedy steps (16-token
+    prompt, then SPLIT_FIRST_TOKEN at n_past 16, ...) whose tokens the split's stream must equal,
+    the digest of the prompt's last logits row, and the per-step logits digests of the
+    teacher-forced pass (oracle_lib.forced_tokens at n_past 16..)"""
     import numpy as np
     import lvk
+    from oracle_lib import forced_tokens
     m = lvk.Llama(path, n_ctx=512)
-    digest = logits_digest(m.eval(np.array(prompt_tokens(16), np.int32), 0)[-1])
+    ptoks = np.array(prompt_tokens(16), np.int32)
+    digest = logits_digest(m.eval(ptoks, 0)[-1])
     tok, out = SPLIT_FIRST_TOKEN, []
     for i in range(n):
         tok = m.eval_greedy(tok, 16 + i)
         out.append(tok)
+    m.eval(ptoks, 0)
+    fdig = [str(lvk.logits_digest(m.eval([int(t)], 16 + i)[-1])) for i, t in enumerate(forced_tokens(SPLIT_FORCED_STEPS))]
     m.close()
-    return out, digest
+    return out, digest, fdig
 
 
 def layer_split(args, coord):
@@ -440,16 +460,21 @@ def layer_split(args, coord):
     pre = coord.max(res["prefill_s"])
     pre0 = coord.max(res["prefill_nomicro_s"])
     digest_split = coord.gather(res.get("prompt_logits_digest"))[-1]     # the last stage's
+    fdig_split = coord.gather(res.get("forced_digests"))[-1]
     check = None
     if rank == 0 and args.split_check > 0:
         n = min(args.split_check, len(res["tokens"]))
         t0 = time.time()
-        want, digest = greedy_tokens_1gpu(path, n)
+        want, digest, fdig = greedy_tokens_1gpu(path, n)
         check = {"n_tokens": n, "tokens_split": res["tokens"][:n], "tokens_1gpu": want,
                  "match": res["tokens"][:n] == want, "check_s": time.time() - t0,
                  "positions": "16..%d" % (16 + n - 1), "first_token": SPLIT_FIRST_TOKEN,
                  "prompt_logits_digest_split": digest_split, "prompt_logits_digest_1gpu": digest,
-                 "prompt_logits_bit_identical": digest_split == digest}
+                 "prompt_logits_bit_identical": digest_split == digest,
+                 "forced_steps": {"n": SPLIT_FORCED_STEPS, "positions": "16..%d" % (15 + SPLIT_FORCED_STEPS),
+                                  "tokens": "oracle_lib.forced_tokens (seeded, non-repeating)",
+                                  "digests_split": fdig_split, "digests_1gpu": fdig,
+                                  "logits_bit_identical_every_step": fdig_split == fdig}}
     coord.barrier()
     L = CFG_65B["n_layer"]
     r = args.steps_split / dec
@@ -558,6 +583,8 @@ def main():
     ap.add_argument("--split-transport", choices=("rccl", "shm"), default="rccl",
                     help="stage link of the layer split: RCCL (one GPU per rank, the default) or the host "
                          "shared-memory ring (ranks may share a GPU: the one-GPU rehearsal)")
+    ap.add_argument("--stream-check", type=int, default=64,
+                    help="teacher-forced steps whose per-step logits digests the chained path must reproduce")
     ap.add_argument("--split-check", type=int, default=16,
                     help="greedy steps of the split replayed on one unsplit context by rank 0 (0: none)")
     ap.add_argument("--split-rehearse", action="store_true",
@@ -570,7 +597,7 @@ def main():
     ap.add_argument("--split-device", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--split-uid", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05_traffic.json"))
     args = ap.parse_args()
     if args.split_child:
         split_child(args)
@@ -614,12 +641,22 @@ def run(args, coord):
     n_ctx = 512
     ptoks = np.array(prompt_tokens(16), np.int32)
 
-    # warmup: prompt + W decode steps (also instantiates the decode graph)
+    # warmup: prompt + W decode steps (also instantiates the decode graph), then the window is
+    # filled once (every position's K / V rows exist before a timed step reads them)
     lg = m.eval(ptoks, 0)
     tok, n_past = int(np.argmax(lg[-1])), 16
     for i in range(args.warmup):
         lg = m.eval([tok], 16 + (i % (n_ctx - 16)))
         tok = int(np.argmax(lg[-1]))
+    lg = m.eval(ptoks, 0)
+    tok = int(np.argmax(lg[-1]))
+    for p in range(16, n_ctx):
+        tok = int(np.argmax(m.eval([tok], p)[-1]))
+    win = n_ctx - 16
+
+    def pos_of(i):
+        # K <= 496: positions spread evenly over 16..511 (K = 496: each once, in order)
+        return 16 + (i * win // args.steps if args.steps <= win else i % win)
 
     # timed region: K greedy decode steps
     lg = m.eval(ptoks, 0)
@@ -627,14 +664,15 @@ def run(args, coord):
     coord.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        lg = m.eval([tok], 16 + (i % (n_ctx - 16)))
+        lg = m.eval([tok], pos_of(i))
         tok = int(np.argmax(lg[-1]))
     t1 = time.perf_counter()
     coord.barrier()
     elapsed = coord.max(t1 - t0)
     value = n_gpus * args.steps / elapsed
-    last = 16 + min(args.steps, n_ctx - 16) - 1
-    positions = "16..%d" % last + ("" if args.steps <= n_ctx - 16 else " (wrapping to 16 after 511)")
+    positions = ("16..511, each once in order" if args.steps == win else
+                 "%d positions spread evenly over 16..511 (window filled first)" % args.steps if args.steps < win else
+                 "16..511 wrapping to 16 after 511")
 
     greedy = None
     if not args.no_greedy:
@@ -676,6 +714,20 @@ def run(args, coord):
                              "path": "lvk_decode_greedy: one call per pass over positions 16..511, the step graph "
                                      "replayed back to back (argmax, step block and next embedding row on the device)",
                              "tokens_match_eval_greedy": seq_c == seq_g}
+        # teacher-forced stream check (a synthetic model's greedy stream settles on one token, so
+        # the check above passes under many numeric errors): seeded non-repeating tokens through
+        # per-step llama_eval and through lvk_decode_chain; every step's device logits digest must
+        # equal the digest of the per-step logits row
+        from oracle_lib import forced_tokens
+        seq_f = forced_tokens(args.stream_check)
+        m.eval(ptoks, 0)
+        want = [lvk.logits_digest(m.eval([int(t)], 16 + i)[-1]) for i, t in enumerate(seq_f)]
+        m.eval(ptoks, 0)
+        _, got = m.decode_chain(seq_f, 16)
+        greedy["stream_check"] = {"steps": len(seq_f), "positions": "16..%d" % (15 + len(seq_f)),
+                                  "tokens": "oracle_lib.forced_tokens (seeded, non-repeating)",
+                                  "digests_equal": got.tolist() == want,
+                                  "first_digests": [hex(d) for d in want[:3]]}
         # host sampler (llama_sample_top_p_top_k, main's defaults: top_k 40, top_p 0.95, temp 0.8,
         # repeat_penalty 1.1 over a 64-token window) on fresh logits (lvk_eval_greedy leaves none)
         m.eval([tok], 16)
@@ -754,6 +806,8 @@ def run(args, coord):
     bpl = prof[dom]["bytes"] / prof[dom]["launches"]
     avg_s = prof[dom]["ms"] / prof[dom]["launches"] * 1e-3
     traffic = None
+    if not os.path.exists(args.traffic_json):     # the previous round's record
+        args.traffic_json = os.path.join(ROOT, "profiles", "r04_traffic.json")
     if os.path.exists(args.traffic_json):
         try:
             traffic = json.load(open(args.traffic_json)).get(dom, {}).get("bytes_per_launch")

@@ -55,8 +55,14 @@ constexpr int SRS = 40, SPL = 8 * SRS, SWF = 4 * SPL;
 // SPLIT: only chunk 0 goes out before the activation table, chunks 1..D-1 after the workgroup
 // barrier (the barriers wait for the slowest wave's issue, which the memory system throttles
 // to the return rate once the CU's queue is full; matvec_cu.hip prologue order 5)
-template <int NW, int D, int PRO, int EPI, int KT, int SPLIT = 0>
+// HALF: the unit of work is a 4-row half group, not an 8-row group: each CU owns an equal share
+// of the 2 G halves and a wave runs two at once (lanes 0-31 and 32-63 read the two 512-byte
+// halves of different groups' 1 KiB slices).  With M = 5120 (13B Wo, W2) every CU then streams
+// exactly 20 rows instead of 16 or 24 (640 groups on 256 CUs).  Not for the W1|W3 epilogue,
+// which pairs the w1 half of a group with its w3 half inside the wave.
+template <int NW, int D, int PRO, int EPI, int KT, int SPLIT = 0, int HALF = 0>
 __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
+    static_assert(!(HALF && EPI == EPI_SWIGLU_F32), "W1|W3 pairs the halves of one group");
     constexpr int nb = KT / 32;                 // blocks per row
     constexpr int nsub = nb / 8;                // 8-block sub-chunks (one uint4 per lane each)
     constexpr int NC = (nb + 31) / 32;          // chunks of 32 blocks
@@ -80,10 +86,27 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     const int j = lane & 7;
     const int r = lane >> 3;
     const int nwg = gridDim.x;
-    const int g0 = (int) (blockIdx.x * (unsigned) P.G / (unsigned) nwg);
-    const int g1 = (int) ((blockIdx.x + 1) * (unsigned) P.G / (unsigned) nwg);
-    const int ng = max(0, (g1 - g0 - wave + NW - 1) / NW);      // row groups of this wave
-    int gc = min(g0 + wave, P.G - 1);
+    // this CU's work items: row groups [i0, i1) (HALF = 0) or half groups [i0, i1) run in pairs
+    const unsigned NI = HALF ? 2u * (unsigned) P.G : (unsigned) P.G;
+    const int i0 = (int) (blockIdx.x * NI / (unsigned) nwg);
+    const int i1 = (int) ((blockIdx.x + 1) * NI / (unsigned) nwg);
+    const int nitems = HALF ? (i1 - i0 + 1) / 2 : i1 - i0;
+    const int ng = max(0, (nitems - wave + NW - 1) / NW);      // work items of this wave
+    // the lane's half group of item k of this CU: unit (g << 1 | hh), g its group, hh the half;
+    // byte offsets of its slices inside a chunk of each image: lp + hh 512 (lanes 32-63 of a
+    // whole group read the second half); a wave without items reads one word (every lane)
+    auto unit_of = [&](int k, bool & valid) __attribute__((always_inline)) {
+        if constexpr (HALF) {
+            const int raw = i0 + 2 * k + (lane >> 5);
+            valid = raw < i1;
+            return min(raw, i1 - 1);
+        } else {
+            valid = true;
+            return 2 * min(i0 + k, P.G - 1) + (lane >> 5);
+        }
+    };
+    const uint32_t lp = (uint32_t) (lane & 31) * 16u;
+    int gc = wave;           // item index of the wave's current row group / half-group pair
 
     // activation inputs first (vmcnt retires in order)
     constexpr bool FPRO = (PRO == PRO_NORM || PRO == PRO_ACTF);
@@ -113,24 +136,35 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
         }
     }
 
-    // first D chunks of this wave's first row group (scalar-base loads)
-    const uint32_t loff = ng > 0 ? (uint32_t) lane * 16u : 0u;
+    // first D chunks of this wave's first item.  Per chunk c of group g the images hold
+    // nib [g][c][4 sub][1 KiB], d | m [g][c][2][1 KiB], wsum [g][c][1 KiB]; a lane's slice of
+    // each 1 KiB is 16 bytes at (hh 512 + lp).  Lane bases per item: lb_n / lb_s / lb_w.
     uint4 W[D][4];
     uint4 WS[D];
     float4 SD[D], SM[D];
-#define LVK_ISSUE41(slot, grp, cc)                                                                      \
+    size_t lb_n, lb_s, lb_w;          // the current item's lane bases
+    auto lane_bases = [&](int k, size_t & bn, size_t & bs, size_t & bw) __attribute__((always_inline)) {
+        bool v;
+        const int u = unit_of(k, v);
+        const size_t gq = (size_t) (u >> 1) * NC;
+        const uint32_t o = ng > 0 ? (uint32_t) (u & 1) * 512u + lp : 0u;
+        bn = gq * 4096 + o;
+        bs = gq * 2048 + o;
+        bw = gq * 1024 + o;
+    };
+    lane_bases(gc, lb_n, lb_s, lb_w);
+#define LVK_ISSUE41(slot, BN, BS, BW, cc)                                                               \
     do {                                                                                                \
-        const uint4 * nb_ = P.nib + ((size_t) (grp) * NC * 4 + (cc) * 4) * 64;                          \
         _Pragma("unroll") for (int sb = 0; sb < 4; ++sb) if ((cc) * 4 + sb < nsub)                      \
-            W[slot][sb] = ld_nt((const uint4 *) ((const char *) (nb_ + sb * 64) + loff));               \
-        const char * sc_ = (const char *) (P.scl + ((size_t) (grp) * NC + (cc)) * 128) + loff;          \
+            W[slot][sb] = ld_nt((const uint4 *) ((const char *) P.nib + (BN) + ((cc) * 4 + sb) * 1024)); \
+        const char * sc_ = (const char *) P.scl + (BS) + (cc) * 2048;                                   \
         SD[slot] = *(const float4 *) sc_;                                                               \
         SM[slot] = *(const float4 *) (sc_ + 1024);                                                      \
-        WS[slot] = ld_nt((const uint4 *) ((const char *) (P.wsum + ((size_t) (grp) * NC + (cc)) * 64) + loff)); \
+        WS[slot] = ld_nt((const uint4 *) ((const char *) P.wsum + (BW) + (cc) * 1024));                 \
         __builtin_amdgcn_sched_barrier(0);                                                              \
     } while (0)
 #pragma unroll
-    for (int d = 0; d < (SPLIT ? 1 : D); ++d) LVK_ISSUE41(d, gc, d);
+    for (int d = 0; d < (SPLIT ? 1 : D); ++d) LVK_ISSUE41(d, lb_n, lb_s, lb_w, d);
 
     // activation table
     if constexpr (FPRO) {
@@ -196,16 +230,18 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     if (ng == 0) return;
     if constexpr (SPLIT) {
 #pragma unroll
-        for (int d = 1; d < D; ++d) LVK_ISSUE41(d, gc, d);
+        for (int d = 1; d < D; ++d) LVK_ISSUE41(d, lb_n, lb_s, lb_w, d);
     }
 
     // row groups: chunk loop with cross-group prefetch
     const bool even = (j & 1) == 0;
     const uint32_t * ys32 = (const uint32_t *) ys;
     float * sw = sbuf + wave * SWF;
-    auto body = [&](auto has_next, int grp, int gnext, float & off) __attribute__((always_inline)) {
+    auto body = [&](auto has_next, float & off) __attribute__((always_inline)) {
         float acc = 0.0f;
         off = 0.0f;
+        size_t nb_n = 0, nb_s = 0, nb_w = 0;        // the next item's lane bases (cross-item prefetch)
+        if constexpr (decltype(has_next)::value) lane_bases(gc + NW, nb_n, nb_s, nb_w);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             const int slot = c % D;
@@ -271,8 +307,8 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
                     }
                 }
             }
-            if (c + D < NC) LVK_ISSUE41(slot, grp, c + D);
-            else if constexpr (decltype(has_next)::value && XG) LVK_ISSUE41(slot, gnext, c + D - NC);
+            if (c + D < NC) LVK_ISSUE41(slot, lb_n, lb_s, lb_w, c + D);
+            else if constexpr (decltype(has_next)::value && XG) LVK_ISSUE41(slot, nb_n, nb_s, nb_w, c + D - NC);
             // chunks stay in program order; the product buffer is rewritten by the next chunk
             asm volatile("" : "+v"(acc), "+v"(off));
             __builtin_amdgcn_wave_barrier();
@@ -281,14 +317,19 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
         return octet_reduce(acc);
     };
 
-    auto epilogue = [&](int grp, float h, float off) __attribute__((always_inline)) {
+    auto epilogue = [&](int item, float h, float off) __attribute__((always_inline)) {
         const float res = h + off * 32.0f;        // acc_offset * QK (ggml.c:2249)
-        const int row = grp * 8 + r;
+        bool valid;
+        const int u = unit_of(item, valid);
+        const int grp = u >> 1;
+        const int row = grp * 8 + (u & 1) * 4 + (r & 3);
         if constexpr (EPI == EPI_STORE) {
-            if (j == 0) P.y[row] = res;
+            if (j == 0 && valid) P.y[row] = res;
         } else if constexpr (EPI == EPI_RESID) {
-            if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+            if (j == 0 && valid) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
         } else if constexpr (EPI == EPI_QKV) {
+            // (a duplicated half, !valid, recomputed its original's rows bit for bit: its stores
+            // write the same values, and the RoPE partner exchange stays convergent)
             const StepParams * sp = P.sp;
             qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32);
         } else if constexpr (EPI == EPI_SWIGLU_F32) {
@@ -305,26 +346,29 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     if constexpr (XG) {
         for (int k = 0; k + 1 < ng; ++k) {
             float off;
-            const float h = body(std::true_type{}, gc, gc + NW, off);
+            const float h = body(std::true_type{}, off);
             epilogue(gc, h, off);
             gc += NW;
+            lane_bases(gc, lb_n, lb_s, lb_w);
         }
     }
     float off;
-    const float h = body(std::false_type{}, gc, gc, off);
+    const float h = body(std::false_type{}, off);
     epilogue(gc, h, off);
 #undef LVK_ISSUE41
 }
 
-template <int NW, int D, int PRO, int EPI, int KT, int SPLIT = 0>
+template <int NW, int D, int PRO, int EPI, int KT, int SPLIT = 0, int HALF = 0>
 hipError_t go(const Cu41Params & P, hipStream_t s) {
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
     constexpr bool XG = (NC % D) == 0;
     const int nwg = std::min(cu_count(), P.G);
-    // without cross-group prefetch every wave must own at most one group
-    if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
+    // work items per CU (row groups, or pairs of half groups): without cross-group prefetch
+    // every wave must own at most one
+    const int items = HALF ? ((2 * P.G + nwg - 1) / nwg + 1) / 2 : (P.G + nwg - 1) / nwg;
+    if (!XG && items > NW) return hipErrorNotSupported;
     const size_t lds = (size_t) nb * 32 + 2 * NC * 128 + (size_t) nb * 16 + NW * SWF * 4 + NW * 8;
-    LVK_LAUNCH((k_mv_cu41<NW, D, PRO, EPI, KT, SPLIT>), dim3(nwg), dim3(NW * 64), lds, s, P);
+    LVK_LAUNCH((k_mv_cu41<NW, D, PRO, EPI, KT, SPLIT, HALF>), dim3(nwg), dim3(NW * 64), lds, s, P);
     return hipGetLastError();
 }
 
@@ -354,6 +398,11 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
     P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx; P.kv32 = L.kv32;
     P.silu_tab = L.silu_tab;
     const int K = L.w.K;
+    // half-group work units (HALF) where they even out the rows per CU: LVK_MV41_HALF=0 restores
+    // whole groups (A/B)
+    static const bool half_env = [] { const char * e = getenv("LVK_MV41_HALF"); return !e || atoi(e) != 0; }();
+    const int nwg = std::min(cu_count(), P.G);
+    const bool half = half_env && P.G % nwg != 0 && (2 * P.G) % nwg == 0;
 #ifdef LVK_PROBE_SWEEP   // dev probe builds only: LVK_CFG41 selects a launch shape (waves, prefetch depth)
     {
         static int cfg = getenv("LVK_CFG41") ? atoi(getenv("LVK_CFG41")) : 0;
@@ -396,18 +445,31 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
         switch (epi) {
             // SPLIT (chunk 1 after the table barrier): 16.9 vs 17.5 us, W2 19.5 vs 19.8
             // (profiles/r03_sweep13_split.txt)
-            case EPI_QKV: if (pro == PRO_NORM) return go<8, 2, PRO_NORM, EPI_QKV, 5120, 1>(P, s); break;
+            case EPI_QKV:
+                if (pro == PRO_NORM) {
+                    if (half) return go<8, 2, PRO_NORM, EPI_QKV, 5120, 1, 1>(P, s);
+                    return go<8, 2, PRO_NORM, EPI_QKV, 5120, 1>(P, s);
+                }
+                break;
             case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<8, 1, PRO_NORM, EPI_SWIGLU_F32, 5120>(P, s); break;
             case EPI_STORE:
                 if (pro == PRO_NORM) return go<8, 1, PRO_NORM, EPI_STORE, 5120>(P, s);
                 if (pro == PRO_ACTF) return go<8, 1, PRO_ACTF, EPI_STORE, 5120>(P, s);
                 break;
-            case EPI_RESID: if (pro == PRO_ACTQ) return go<3, 2, PRO_ACTQ, EPI_RESID, 5120>(P, s); break;
+            case EPI_RESID:
+                if (pro == PRO_ACTQ) {
+                    if (half) return go<3, 2, PRO_ACTQ, EPI_RESID, 5120, 0, 1>(P, s);
+                    return go<3, 2, PRO_ACTQ, EPI_RESID, 5120>(P, s);
+                }
+                break;
         }
     } else if (K == 13824) {
         // 8 waves: the 5-6 without a row group help quantize u (r03 sweep: 19.9 vs 20.9 us;
         // D = 7 / 14 with 4 waves: 23.5 / 28.3)
-        if (epi == EPI_RESID && pro == PRO_ACTF) return go<8, 2, PRO_ACTF, EPI_RESID, 13824, 1>(P, s);
+        if (epi == EPI_RESID && pro == PRO_ACTF) {
+            if (half) return go<8, 2, PRO_ACTF, EPI_RESID, 13824, 1, 1>(P, s);
+            return go<8, 2, PRO_ACTF, EPI_RESID, 13824, 1>(P, s);
+        }
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<4, 2, PRO_ACTF, EPI_STORE, 13824>(P, s);
     } else if (K == 4096) {
         switch (epi) {

@@ -131,6 +131,8 @@ def test_7b_shaped_decode_vs_oracle(lvk, oracle, model_dir, n_prompt):
     om.close()
 
 
+@pytest.mark.parametrize("cfg,steps", [(dict(n_embd=5120, n_head=40, n_layer=2, seed=11), 12),
+                                       (dict(n_embd=4096, n_head=32, n_layer=2, seed=12), 8)])
 def test_q4_1_shaped_decode_vs_oracle(lvk, oracle, model_dir, cfg, steps):
     """LLaMA-13B (n_embd 5120, n_ff 13824, 40 heads) and 7B layer shapes in Q4_1, 2 layers:
     Q4_1 quantizer, the CU-balanced Q4_1 decode matvecs (matvec_cu41.hip: QKV + RoPE, Wo,

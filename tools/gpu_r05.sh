@@ -5,6 +5,7 @@
 #   diag65      the 65B decode under rocprofv3 --kernel-trace with LVK_SEGV_TRACE=1 (native frames
 #               and /proc/self/maps on a fault)                      -> gpurun_out/r05_diag65/
 #   prof65      the same trace, expected to complete                 -> gpurun_out/r05_prof65/
+#   ab13        13B Q4_1 decode with and without half-group work units -> gpurun_out/r05_ab13/
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -28,6 +29,15 @@ for step in "$@"; do
       done
     done
     cat $O/xcc.log; grep -h mode $O/*.log ;;
+  ab13)
+    # 13B Q4_1 decode: half-group work units (LVK_MV41_HALF) A/B, twice each
+    O=gpurun_out/r05_ab13; mkdir -p $O
+    for r in 1 2; do
+      for h in 0 1; do
+        LVK_MV41_HALF=$h timeout -k 10 300 python3 tools/decode_speed.py 13b 64 2>/dev/null \
+          | sed "s/^{/{\"half\": $h, /" | tee -a $O/ab.jsonl || exit 41
+      done
+    done ;;
   diag65)
     O=gpurun_out/r05_diag65; mkdir -p $O
     timeout -k 10 600 python3 tools/decode_speed.py 65b 4 > $O/gen.log 2>&1 || exit 21
