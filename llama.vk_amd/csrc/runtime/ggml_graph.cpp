@@ -606,9 +606,15 @@ size_t span_bytes(const ggml_tensor * t) {
 //     (/proc/self/pagemap bit 55, cleared by "4" into /proc/self/clear_refs; a new mapping
 //     reads dirty, a page that is neither present nor swapped counts as written), and are
 //     uploaded again on every call where they do not;
+//   * pages the CPU-side tracking cannot see written are never kept: pages of shared mappings
+//     (another mapping or process may write them; HIP's pinned host allocations are shared
+//     mappings of the driver's device file) and host memory registered with HIP (a DMA into
+//     it, e.g. hipMemcpy D2H, bypasses this process's page tables) are uploaded on every call;
 //   * only bytes a node reads before any node of the call writes them are uploaded at all
 //     (a node's output buffer never travels host -> device), and only the bytes the nodes
 //     wrote travel back.
+// The soft-dirty bits are per process: before a call clears them, every engine (one per
+// device) folds the bits into the validity of all its mirrors.
 // LVK_GGML_CACHE=0 turns the caching off (every needed page uploaded on every call).
 constexpr size_t PAGE = 4096;
 
@@ -703,6 +709,7 @@ struct Mirror {
     std::vector<uint8_t> valid;
     std::vector<int32_t> ro;       // per page: the read-only mapping it was uploaded from, or -1
     uint64_t last_call = 0;
+    int hip_host = -1;             // 1: HIP-registered / pinned host memory (never cached); -1 unknown
     uintptr_t page0() const { return (uintptr_t) lo / PAGE; }
     size_t pages() const { return (uintptr_t) (hi - 1) / PAGE - page0() + 1; }
 };
@@ -859,15 +866,34 @@ struct GraphEngine {
     void refresh_validity(Mirror & m) {
         DirtyTracker & T = tracker();
         if (!T.enabled) { std::fill(m.valid.begin(), m.valid.end(), 0); return; }
+        // host memory HIP can DMA into (registered or pinned): no CPU-side tracking sees those writes
+        if (m.hip_host < 0) {
+            hipPointerAttribute_t a{};
+            const bool lo_host = hipPointerGetAttributes(&a, m.lo) == hipSuccess && a.type == hipMemoryTypeHost;
+            (void) hipGetLastError();
+            hipPointerAttribute_t b{};
+            const bool hi_host = hipPointerGetAttributes(&b, m.hi - 1) == hipSuccess && b.type == hipMemoryTypeHost;
+            (void) hipGetLastError();
+            m.hip_host = lo_host || hi_host ? 1 : 0;
+        }
+        if (m.hip_host == 1) { std::fill(m.valid.begin(), m.valid.end(), 0); return; }
         if (T.ok) {
             std::vector<uint64_t> e;
             if (!T.read(m.page0(), m.pages(), e)) { std::fill(m.valid.begin(), m.valid.end(), 0); return; }
             for (size_t i = 0; i < e.size(); ++i)
                 if (DirtyTracker::written(e[i])) m.valid[i] = 0;
-            return;
+        } else {
+            for (size_t i = 0; i < m.valid.size(); ++i)
+                if (m.ro[i] < 0 || !ro_alive[(size_t) m.ro[i]]) m.valid[i] = 0;
         }
-        for (size_t i = 0; i < m.valid.size(); ++i)
-            if (m.ro[i] < 0 || !ro_alive[(size_t) m.ro[i]]) m.valid[i] = 0;
+        // pages of shared mappings (or of no mapping this call saw) are written behind our back
+        auto it = maps_now.begin();
+        for (size_t i = 0; i < m.valid.size(); ++i) {
+            if (!m.valid[i]) continue;
+            const uintptr_t a = (m.page0() + i) * PAGE;
+            while (it != maps_now.end() && it->hi <= a) ++it;
+            if (it == maps_now.end() || a < it->lo || it->perms[3] == 's') m.valid[i] = 0;
+        }
     }
     int32_t ro_id(uintptr_t page) {
         const MapEnt * e = map_of(maps_now, page * PAGE);
@@ -969,8 +995,12 @@ std::mutex & engine_mutex() {
     static std::mutex m;
     return m;
 }
-GraphEngine & engine() {
+std::map<int, GraphEngine *> & all_engines() {
     static std::map<int, GraphEngine *> per_dev;
+    return per_dev;
+}
+GraphEngine & engine() {
+    std::map<int, GraphEngine *> & per_dev = all_engines();
     int d = 0;
     LVK_HIP(hipGetDevice(&d));
     auto it = per_dev.find(d);
@@ -1210,7 +1240,7 @@ extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph
             }
         }
         DirtyTracker & T = tracker();
-        if (T.enabled && !T.ok) R.snapshot_maps();
+        if (T.enabled) R.snapshot_maps();
         for (Mirror * m : R.used) R.refresh_validity(*m);
         // the bytes a node reads before any earlier node of this call wrote them (leaves, the
         // caller's inputs, a KV cache) are the only ones that must come from the host
@@ -1276,7 +1306,6 @@ extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph
             R.last.d2h += (uint64_t) (w.hi - w.lo);
         }
         LVK_HIP(hipStreamSynchronize(R.stream));
-        // mirrors this call did not use: note their host writes before the bits are cleared;
         // mirrors unused for 8 calls are freed (a caller's per-call scratch contexts)
         for (size_t i = 0; i < R.mirrors.size();) {
             Mirror * m = R.mirrors[i];
@@ -1287,12 +1316,22 @@ extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph
                 delete m;
                 continue;
             }
-            if (m->last_call != R.calls && T.ok) R.refresh_validity(*m);
             ++i;
         }
-        if (T.ok && !T.clear()) {
-            T.ok = false;
-            for (Mirror * m : R.mirrors) std::fill(m->valid.begin(), m->valid.end(), 0);
+        // the soft-dirty bits are process-wide: every engine's mirrors this call did not use
+        // (all those of the other devices' engines) note their host writes before the clear
+        if (T.ok) {
+            for (auto & kv : all_engines()) {
+                GraphEngine & E = *kv.second;
+                if (&E != &R) E.maps_now = R.maps_now;
+                for (Mirror * m : E.mirrors)
+                    if (&E != &R || m->last_call != R.calls) E.refresh_validity(*m);
+            }
+            if (!T.clear()) {
+                T.ok = false;
+                for (auto & kv : all_engines())
+                    for (Mirror * m : kv.second->mirrors) std::fill(m->valid.begin(), m->valid.end(), 0);
+            }
         }
         uint64_t resident = 0;
         for (Mirror * m : R.mirrors) resident += (uint64_t) (m->hi - m->lo);
@@ -1320,16 +1359,19 @@ extern "C" int lvk_ggml_invalidate(const void * p, size_t n) {
     std::lock_guard<std::mutex> lock(engine_mutex());
     if (!p) return -1;
     try {
-        GraphEngine & R = engine();
+        // every device's engine may mirror the range
         const char * a = (const char *) p;
         const char * b = a + n;
-        for (Mirror * m : R.mirrors) {
-            if (!overlaps(a, b, m->lo, m->hi)) continue;
-            const size_t i0 = (uintptr_t) std::max(a, (const char *) m->lo) / PAGE - m->page0();
-            const size_t i1 = (uintptr_t) (std::min(b, (const char *) m->hi) - 1) / PAGE - m->page0() + 1;
-            for (size_t i = i0; i < i1; ++i) m->valid[i] = 0;
+        for (auto & kv : all_engines()) {
+            GraphEngine & R = *kv.second;
+            for (Mirror * m : R.mirrors) {
+                if (!overlaps(a, b, m->lo, m->hi)) continue;
+                const size_t i0 = (uintptr_t) std::max(a, (const char *) m->lo) / PAGE - m->page0();
+                const size_t i1 = (uintptr_t) (std::min(b, (const char *) m->hi) - 1) / PAGE - m->page0() + 1;
+                for (size_t i = i0; i < i1; ++i) m->valid[i] = 0;
+            }
+            R.drop_repacked(a, b);
         }
-        R.drop_repacked(a, b);
     } catch (const lvk::Error & e) {
         fprintf(stderr, "lvk_ggml_invalidate: %s\n", e.msg.c_str());
         return -1;

@@ -66,3 +66,17 @@ def test_graph_compute_uploads_weights_once(gpu_available, wtype, tmp_path):
         assert c["d2h"] < wbytes / 4, calls
         assert c["mode"] in (1, 2), calls
     print("per-call ms:", [round(c["ms"], 3) for c in calls], "h2d:", [int(c["h2d"]) for c in calls])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["private", "pinned", "shared"])
+def test_graph_compute_sees_untracked_host_writes(gpu_available, mode):
+    """the mirrors must not keep a stale device copy of host bytes that change where the CPU
+    page tables cannot see it between two calls: a hipMemcpy D2H (DMA) into a pinned context
+    buffer, a write through a second MAP_SHARED view of the buffer's pages, and (the tracked
+    case) a plain CPU write (tools/ggml_graph/volatile_test.cpp: z = x + y checked after each)"""
+    b = os.path.join(os.path.dirname(LVK_BIN), "volatile_test")
+    if not os.path.exists(b):
+        subprocess.check_call(["make", "-C", os.path.dirname(os.path.dirname(b))], stdout=subprocess.DEVNULL)
+    r = subprocess.run([b, mode], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and ("ok %s" % mode) in r.stdout, r.stderr[-2000:]
