@@ -317,6 +317,7 @@ struct ShmHeader {
     uint32_t n_stages;
     uint32_t slots;
     uint64_t slot_bytes;
+    std::atomic<uint32_t> go;          // set by stage 0 once all S stages have joined this object
 };
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory rings need address-free atomics");
 constexpr size_t SHM_DATA_OFF = 4096;
@@ -377,6 +378,7 @@ struct ShmTransport final : StageTransport {
         h->slot_bytes = slot;
         h->joined.store(0, std::memory_order_relaxed);
         h->abort.store(0, std::memory_order_relaxed);
+        h->go.store(0, std::memory_order_relaxed);
         h->magic.store(SHM_MAGIC, std::memory_order_release);
     }
     // stages 1..S-1: map the object once it exists and is initialised; false = try again
@@ -417,6 +419,7 @@ struct ShmTransport final : StageTransport {
             create();
             h->joined.fetch_add(1, std::memory_order_acq_rel);
             spin_until([&] { return h->joined.load(std::memory_order_acquire) >= (uint32_t) S; }, "joining");
+            h->go.store(1, std::memory_order_release);  // the joiners wait for this, not for the count
             shm_unlink(shm_name.c_str());             // every stage has mapped it
             named = false;
             return;
@@ -424,9 +427,11 @@ struct ShmTransport final : StageTransport {
         for (int i = 0;; ++i) {
             ino_t ino = 0;
             if (try_open(ino)) {
-                h->joined.fetch_add(1, std::memory_order_acq_rel);
-                bool stale = false;
-                for (int k = 0; h->joined.load(std::memory_order_acquire) < (uint32_t) S; ++k) {
+                // an object a dead stage 0 left behind may already count S - 1 or more joins:
+                // the join completes only when a live stage 0 sets `go`, and a count already at
+                // S means the object belonged to a completed (dead) connect
+                bool stale = h->joined.fetch_add(1, std::memory_order_acq_rel) >= (uint32_t) S;
+                for (int k = 0; !stale && !h->go.load(std::memory_order_acquire); ++k) {
                     if (h->abort.load(std::memory_order_acquire)) throw Error("llama.vk_amd: stage link aborted by a peer (joining)");
                     if (since_s(t0) > limit) { abort(); throw Error("llama.vk_amd: stage link timed out (joining)"); }
                     if ((k & 255) == 255 && replaced(ino)) { stale = true; break; }
