@@ -509,6 +509,262 @@ hipError_t go(const CuParams & P, hipStream_t s) {
     return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// K-split decode matvec (k_mv_ks): the per-wave chain, not the weight stream, sets the time of a
+// decode matvec whose CU owns only a few row groups (7B Wo / W2: 2 groups per CU, one wave each
+// running 128 / 344 blocks in order, ~28 cycles per block; tools/probe traces).  Only the fp32
+// FMA of each block is serial in the reference's chain (acc_j = fmaf(s_b, P_bj, acc_j) in block
+// order, ggml.c:2013); the integer partials P_bj and the scale products s_b are not.  So each row
+// group is cut into S segments of consecutive 8-block sub-chunks, one wave per segment: every wave
+// loads its segment's weights, computes its P (v_dot8, exact integers |P| <= 256 kept as f16) and s
+// (= dw * dx, f32) into registers while the others do the same, and then the segments' FMAs run
+// in order as a baton: wave k waits for wave k-1's 64 chain values in LDS, continues the chains
+// with v_fma_mix (f32 s, f16 P: fmaf(s, (float) P, acc), one rounding), and hands them on.  The
+// last segment's wave reduces (AVX2 horizontal order) and runs the epilogue.  Bit-identical to
+// k_mv_cu by construction: the same FMAs in the same order.
+template <int S, int GMAX, int PRO, int EPI, int KT>
+__global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
+    constexpr int NW = S * GMAX;
+    constexpr int NT = NW * 64;
+    constexpr int nb = KT / 32;
+    constexpr int nsub = nb / 8;                 // 8-block sub-chunks of a row
+    constexpr int NC = (nb + 31) / 32;
+    constexpr int SEG = (nsub + S - 1) / S;      // sub-chunks per segment (at most)
+    constexpr int SC = SEG / 4 + 2;              // chunks a segment can touch
+    constexpr int nunits = KT / 8;
+    constexpr bool FPRO = (PRO == PRO_NORM || PRO == PRO_ACTF);
+    static_assert(nb % 8 == 0, "K must be a multiple of 256");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t * act = (uint32_t *) smem;                          // nb * 32 B
+    float * dxp = (float *) (smem + nb * 32);                    // NC * 128 B
+    float * sbuf = dxp + NC * 32;                                // NW * SPL floats (one table per wave)
+    float * bacc = sbuf + NW * SPL;                              // GMAX * 64 chain values (the baton)
+    unsigned * bflag = (unsigned *) (bacc + GMAX * 64);          // GMAX baton words
+    double * red = (double *) (bflag + GMAX + (GMAX & 1));       // NW doubles
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 7, r = lane >> 3;
+    const int gi = wave / S, seg = wave - gi * S;              // this wave's row group and segment
+    const int g0 = (int) ((unsigned) blockIdx.x * (unsigned) P.G / (unsigned) gridDim.x);
+    const int g1 = (int) ((unsigned) (blockIdx.x + 1) * (unsigned) P.G / (unsigned) gridDim.x);
+    const bool has = g0 + gi < g1;
+    const int grp = min(g0 + gi, P.G - 1);
+    const int u0 = seg * nsub / S, u1 = (seg + 1) * nsub / S;  // sub-chunks [u0, u1)
+    const int c0 = u0 >> 2;                                    // first chunk touched
+
+    // 1. the prologue inputs, then this segment's weights and scales, all in flight at once
+    constexpr int UM = FPRO ? (nunits + NT - 1) / NT : (nb + NT - 1) / NT;
+    float4 xv[UM][2];
+    float4 gv[PRO == PRO_NORM ? UM : 1][2];
+    uint4 qv[FPRO ? 1 : UM];
+    float dv[FPRO ? 1 : UM];
+    if constexpr (FPRO) {
+#pragma unroll
+        for (int k = 0; k < UM; ++k) {
+            const int un = min(k * NT + tid, nunits - 1);
+            const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
+            xv[k][0] = xp[0]; xv[k][1] = xp[1];
+            if constexpr (PRO == PRO_NORM) {
+                const float4 * gp = (const float4 *) (P.g + (size_t) un * 8);
+                gv[k][0] = gp[0]; gv[k][1] = gp[1];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < UM; ++k) {
+            const int b = min(k * NT + tid, nb - 1);
+            qv[k] = P.xq.qs[b];
+            dv[k] = P.xq.d[b];
+        }
+    }
+    const uint32_t loff = has ? (uint32_t) lane * 16u : 0u;
+    uint4 W[SEG];
+    float4 SS[SC];
+#pragma unroll
+    for (int i = 0; i < SC; ++i) {
+        const int c = min(c0 + i, NC - 1);
+        SS[i] = *(const float4 *) ((const char *) (P.scl + ((size_t) grp * NC + c) * 64) + loff);
+    }
+#pragma unroll
+    for (int i = 0; i < SEG; ++i) {
+        const int u = min(u0 + i, nsub - 1);
+        W[i] = ld_nt((const uint4 *) ((const char *) (P.nib + ((size_t) grp * NC * 4 + u) * 64) + loff));
+    }
+#pragma unroll
+    for (int k = 0; k < UM; ++k) {
+        if constexpr (FPRO) {
+            launder(xv[k][0]); launder(xv[k][1]);
+            if constexpr (PRO == PRO_NORM) { launder(gv[k][0]); launder(gv[k][1]); }
+        } else {
+            launder(qv[k]); launder(dv[k]);
+        }
+    }
+    if (tid < GMAX) bflag[tid] = 0u;
+
+    // 2. the activation table (every wave builds its share; matvec_common.h layout)
+    if constexpr (FPRO) {
+        float scale = 1.0f;
+        if constexpr (PRO == PRO_NORM) {
+            // ggml_compute_forward_rms_norm_f32 (ggml.c:6058-6076), as mv_cu_run
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < UM; ++k) {
+                if (k * NT + tid < nunits) {
+                    const float e[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
+                                        xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) { const float sq = e[q] * e[q]; acc += (double) sq; }
+                }
+            }
+            acc = wave_sum_d(acc);
+            if (lane == 0) red[wave] = acc;
+            __syncthreads();
+            double sum = red[0];
+            for (int w = 1; w < NW; ++w) sum += red[w];
+            const float mean = (float) (sum / (double) KT);
+            scale = 1.0f / sqrtf(mean + 1e-6f);
+        }
+#pragma unroll
+        for (int k = 0; k < UM; ++k) {
+            if (k * NT >= nunits) break;
+            const int un = k * NT + tid;
+            float v[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
+                          xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
+            float amax = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                if constexpr (PRO == PRO_NORM) {
+                    const float gg[8] = {gv[k][0].x, gv[k][0].y, gv[k][0].z, gv[k][0].w,
+                                         gv[k][1].x, gv[k][1].y, gv[k][1].z, gv[k][1].w};
+                    const float yn = v[e] * scale;      // ggml_vec_scale_f32 (ggml.c:6076)
+                    v[e] = gg[e] * yn;                  // ggml_mul(repeat(g), cur) (llama.cpp:984)
+                }
+                const float a = fabsf(v[e]);
+                amax = a > amax ? a : amax;
+            }
+            const float o0 = quad_bcast<0>(amax), o1 = quad_bcast<1>(amax);
+            const float o2 = quad_bcast<2>(amax), o3 = quad_bcast<3>(amax);
+            const float m01 = o1 > o0 ? o1 : o0, m23 = o3 > o2 ? o3 : o2;
+            amax = m23 > m01 ? m23 : m01;
+            const float d = amax / 7.0f;                              // ggml.c:651
+            const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;     // ggml.c:653
+            const uint32_t w = q40_pack8(v, id);
+            if (un < nunits) act_store(act, dxp, un >> 2, un & 3, w, d, (un & 3) == 0);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < UM; ++k) {
+            const int b = k * NT + tid;
+            if (b < nb) {
+                act_store(act, dxp, b, 0, qv[k].x, dv[k], true);
+                act_store(act, dxp, b, 1, qv[k].y, 0.0f, false);
+                act_store(act, dxp, b, 2, qv[k].z, 0.0f, false);
+                act_store(act, dxp, b, 3, qv[k].w, 0.0f, false);
+            }
+        }
+    }
+    __syncthreads();            // activation table and baton words ready
+    if (!has) return;
+
+    // 3. this segment's partials P (f16 pairs) and scale products s, chunk by chunk
+    uint32_t PH[SEG * 4];        // P of blocks 8i + 2t, 8i + 2t + 1 (halves) for sub-chunk i
+    float SV[SEG * 8];           // s of block 8i + t
+    float * sw = sbuf + wave * SPL;
+#pragma unroll
+    for (int i = 0; i < SEG; ++i) {
+        const int u = u0 + i;
+        if (u < u1) {
+            const int c = u >> 2;
+            if (i == 0 || (u & 3) == 0) {
+                // the scale table of chunk c: s = dw * dx of blocks 32c + 8m + j (ggml.c:1968)
+                const float4 dx = *(const float4 *) (dxp + c * 32 + j * 4);
+                const int ci = c - c0;             // (selects, not a dynamic register index)
+                float4 dw = SS[0];
+#pragma unroll
+                for (int k = 1; k < SC; ++k) if (ci == k) dw = SS[k];
+                *(float4 *) (sw + r * SRS + j * 4) = make_float4(dw.x * dx.x, dw.y * dx.y, dw.z * dx.z, dw.w * dx.w);
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+            // blocks 8 (u & 3) + t of chunk c: table slot 4 t' + m with block 8m + t'
+            const int sb = u & 3;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) SV[i * 8 + t] = sw[r * SRS + t * 4 + sb];
+            const uint32_t wd[4] = {W[i].x, W[i].y, W[i].z, W[i].w};
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+                const uint4 a = *(const uint4 *) (act + ((size_t) (u * 2 + pp) * 8 + j) * 4);
+                const int p0 = dot8(wd[2 * pp], a.x), p1 = dot8(wd[2 * pp], a.y);
+                const int p2 = dot8(wd[2 * pp + 1], a.z), p3 = dot8(wd[2 * pp + 1], a.w);
+                PH[i * 4 + pp * 2] = (uint32_t) f16_bits_i(p0) | ((uint32_t) f16_bits_i(p1) << 16);
+                PH[i * 4 + pp * 2 + 1] = (uint32_t) f16_bits_i(p2) | ((uint32_t) f16_bits_i(p3) << 16);
+            }
+            if ((u & 3) == 3) __builtin_amdgcn_wave_barrier();   // the table is rewritten next chunk
+        }
+    }
+
+    // 4. the baton: segment seg continues the chains of segment seg - 1
+    float acc = 0.0f;
+    if (seg > 0) {
+        unsigned * fl = bflag + gi;
+        bool ok = true;
+        for (int spins = 0; __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (unsigned) seg; ++spins) {
+            if (spins > (1 << 22)) { ok = false; break; }    // never expected: poison the rows
+            __builtin_amdgcn_s_sleep(1);
+        }
+        acc = ok ? bacc[gi * 64 + lane] : __builtin_nanf("");
+    }
+#pragma unroll
+    for (int i = 0; i < SEG; ++i) {
+        if (u0 + i < u1) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                acc = fma_mix_f32_f16<0>(SV[i * 8 + 2 * t], PH[i * 4 + t], acc);
+                acc = fma_mix_f32_f16<1>(SV[i * 8 + 2 * t + 1], PH[i * 4 + t], acc);
+            }
+        }
+    }
+    if (seg + 1 < S) {
+        bacc[gi * 64 + lane] = acc;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(bflag + gi, (unsigned) (seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+    }
+    const float res = octet_reduce(acc);
+    const int row = grp * 8 + r;
+    if constexpr (EPI == EPI_STORE) {
+        if (j == 0) P.y[row] = res;
+    } else if constexpr (EPI == EPI_RESID) {
+        if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+    } else if constexpr (EPI == EPI_QKV) {
+        const StepParams * sp = P.sp;
+        qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32);
+    } else if constexpr (EPI == EPI_SWIGLU_F32) {
+        const float a3 = __shfl_xor(res, 32);
+        if (r < 4 && j == 0) {
+            const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res)]);   // ggml_vec_silu_f32 (ggml.c:2495)
+            P.u[grp * 4 + r] = sl * a3;                                  // ggml_mul (llama.cpp:1096)
+        }
+    }
+}
+
+template <int S, int GMAX, int PRO, int EPI, int KT>
+hipError_t go_ks(const CuParams & P, hipStream_t s) {
+    constexpr int nb = KT / 32, NC = (nb + 31) / 32, NW = S * GMAX;
+    const int nwg = std::min(cu_count(), P.G);
+    if ((P.G + nwg - 1) / nwg > GMAX) return hipErrorNotSupported;
+    const size_t lds = (size_t) nb * 32 + NC * 128 + (size_t) NW * SPL * 4 + GMAX * 64 * 4 + (GMAX + (GMAX & 1)) * 4 + NW * 8;
+    LVK_LAUNCH((k_mv_ks<S, GMAX, PRO, EPI, KT>), dim3(nwg), dim3(NW * 64), lds, s, P);
+    return hipGetLastError();
+}
+
+// LVK_MV_KS=0 keeps the one-wave-per-row-group kernel for every shape (A/B)
+static bool ks_env() {
+    static const bool v = [] { const char * e = getenv("LVK_MV_KS"); return !e || atoi(e) != 0; }();
+    return v;
+}
 }  // namespace
 
 // CUs of the current device, cached per device id (a one-process layer split may drive
@@ -586,7 +842,15 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
             case EPI_QKV: if (pro == PRO_NORM) return go<8, 0, 2, PRO_NORM, EPI_QKV, 4096, 5>(P, s); break;
             case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 4096, 5>(P, s); break;
             case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 4096, 1>(P, s); break;
-            case EPI_RESID: if (pro == PRO_ACTQ) return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096, 5>(P, s); break;
+            case EPI_RESID:
+                if (pro == PRO_ACTQ) {
+                    if (ks_env()) {
+                        const hipError_t e = go_ks<4, 2, PRO_ACTQ, EPI_RESID, 4096>(P, s);
+                        if (e != hipErrorNotSupported) return e;
+                    }
+                    return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096, 5>(P, s);
+                }
+                break;
         }
         // operator API (lvk_mul_mat_q: plain quantize of an f32 input)
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 4096>(P, s);
@@ -606,6 +870,10 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         // profiles/r03_np_sweep.txt: 7.0 us against 8.6-9.3 for 8 waves that all quantize u
         // and then issue the weights)
         if (epi == EPI_RESID && pro == PRO_ACTF) {
+            if (ks_env()) {
+                const hipError_t e = go_ks<6, 2, PRO_ACTF, EPI_RESID, 11008>(P, s);
+                if (e != hipErrorNotSupported) return e;
+            }
             // (needs at most 2 row groups per CU: a device with fewer CUs takes 8 waves that
             // all quantize u, then issue the weights)
             const hipError_t e = go<2, 6, 4, PRO_ACTF, EPI_RESID, 11008, 0>(P, s);

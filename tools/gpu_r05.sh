@@ -9,6 +9,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
 T="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
 
 for step in "$@"; do
@@ -50,6 +51,33 @@ for step in "$@"; do
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
       python3 tools/decode_speed.py 65b 16 > $O/kt65.log 2>&1 || exit 32
     find $O -name '*kernel_stats.csv' ;;
+  ks)
+    # the K-split decode matvec (Wo, W2): parity of the 7B-shaped / full 7B decode, then A/B speed
+    O=gpurun_out/r05_ks; mkdir -p $O
+    timeout -k 10 900 $T tests/test_gpu_model.py tests/test_gpu_decode_chain.py tests/test_gpu_7b_full.py \
+      > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 51; }
+    tail -2 $O/tests.log
+    for r in 1 2; do
+      for k in 0 1; do
+        LVK_MV_KS=$k timeout -k 10 300 python3 tools/decode_speed.py 7b 96 2>/dev/null \
+          | sed "s/^{/{\"ks\": $k, /" | tee -a $O/ab.jsonl || exit 52
+      done
+    done ;;
+  trace)
+    # per-wave phase stamps of the decode matvecs (tools/probe/mv_probe_T: kinds 0 qkv, 2 wo, 3 w13, 4 w2)
+    O=gpurun_out/r05_trace; mkdir -p $O
+    for k in 0 2 3 4; do
+      LVK_TRACE_KIND=$k timeout -k 10 120 ./tools/probe/mv_probe_T 256 > $O/trace_$k.log 2>&1 || exit 61
+    done
+    grep -h "trace kind\|chunk  0\|workgroup end" $O/trace_*.log ;;
+  diag04)
+    # the round-4 library (lib/r04diag, built from commit 7eefa8d + the maps dump) under the
+    # kernel trace that crashed in round 4
+    O=gpurun_out/r05_diag04; mkdir -p $O
+    timeout -k 10 600 python3 tools/decode_speed.py 65b 4 > $O/gen.log 2>&1 || exit 71
+    LVK_SEGV_TRACE=1 LVK_LIB=$R/llama.vk_amd/lib/r04diag/libllama_vk_amd.so timeout -k 10 600 rocprofv3 --kernel-trace \
+      --stats -d $O/kt -o run --output-format csv -- python3 tools/r04diag/decode_speed.py 65b 16 > $O/kt65.log 2>&1
+    rc=$?; grep -v "^[EW]2026" $O/kt65.log | head -20; exit $rc ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done
