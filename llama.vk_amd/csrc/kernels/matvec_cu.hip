@@ -546,6 +546,7 @@ __global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int j = lane & 7, r = lane >> 3;
+    LVK_T(0);
     const int gi = wave / S, seg = wave - gi * S;              // this wave's row group and segment
     const int g0 = (int) ((unsigned) blockIdx.x * (unsigned) P.G / (unsigned) gridDim.x);
     const int g1 = (int) ((unsigned) (blockIdx.x + 1) * (unsigned) P.G / (unsigned) gridDim.x);
@@ -602,6 +603,7 @@ __global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
         }
     }
     if (tid < GMAX) bflag[tid] = 0u;
+    LVK_T(1);
 
     // 2. the activation table (every wave builds its share; matvec_common.h layout)
     if constexpr (FPRO) {
@@ -666,6 +668,7 @@ __global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
         }
     }
     __syncthreads();            // activation table and baton words ready
+    LVK_T(2);
     if (!has) return;
 
     // 3. this segment's partials P (f16 pairs) and scale products s, chunk by chunk
@@ -704,6 +707,7 @@ __global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
             if ((u & 3) == 3) __builtin_amdgcn_wave_barrier();   // the table is rewritten next chunk
         }
     }
+    LVK_T(3);
 
     // 4. the baton: segment seg continues the chains of segment seg - 1
     float acc = 0.0f;
@@ -716,6 +720,7 @@ __global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
         }
         acc = ok ? bacc[gi * 64 + lane] : __builtin_nanf("");
     }
+    LVK_T(4);
 #pragma unroll
     for (int i = 0; i < SEG; ++i) {
         if (u0 + i < u1) {
@@ -727,12 +732,14 @@ __global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
         }
     }
     if (seg + 1 < S) {
+        LVK_T(5);
         bacc[gi * 64 + lane] = acc;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store(bflag + gi, (unsigned) (seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return;
     }
     const float res = octet_reduce(acc);
+    LVK_T(5);
     const int row = grp * 8 + r;
     if constexpr (EPI == EPI_STORE) {
         if (j == 0) P.y[row] = res;

@@ -398,9 +398,11 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
     P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx; P.kv32 = L.kv32;
     P.silu_tab = L.silu_tab;
     const int K = L.w.K;
-    // half-group work units (HALF) where they even out the rows per CU: LVK_MV41_HALF=0 restores
-    // whole groups (A/B)
-    static const bool half_env = [] { const char * e = getenv("LVK_MV41_HALF"); return !e || atoi(e) != 0; }();
+    // half-group work units (HALF) where they even out the rows per CU: opt-in (LVK_MV41_HALF=1).
+    // Measured on 13B (profiles/r05_ab13.jsonl): 312.1 / 312.4 tok/s against 319.3 / 312.0 with
+    // whole groups, Wo 7.4 vs 6.9-7.3 us, W2 19.3 vs 18.9-19.5 us -- the 20 % byte imbalance of
+    // M = 5120 is not what sets these kernels' time (each wave's serial chain is)
+    static const bool half_env = [] { const char * e = getenv("LVK_MV41_HALF"); return e && atoi(e) != 0; }();
     const int nwg = std::min(cu_count(), P.G);
     const bool half = half_env && P.G % nwg != 0 && (2 * P.G) % nwg == 0;
 #ifdef LVK_PROBE_SWEEP   // dev probe builds only: LVK_CFG41 selects a launch shape (waves, prefetch depth)

@@ -64,12 +64,16 @@ for step in "$@"; do
       done
     done ;;
   trace)
-    # per-wave phase stamps of the decode matvecs (tools/probe/mv_probe_T: kinds 0 qkv, 2 wo, 3 w13, 4 w2)
+    # per-wave phase stamps of the decode matvecs (tools/probe/mv_probe_T, LVK_TRACE_RAW: events per
+    # wave index), kinds 2 wo, 4 w2, with and without the K-split kernel
     O=gpurun_out/r05_trace; mkdir -p $O
-    for k in 0 2 3 4; do
-      LVK_TRACE_KIND=$k timeout -k 10 120 ./tools/probe/mv_probe_T 256 > $O/trace_$k.log 2>&1 || exit 61
+    for k in 2 4; do
+      for ks in 0 1; do
+        LVK_MV_KS=$ks LVK_TRACE_RAW=1 LVK_TRACE_KIND=$k timeout -k 10 120 ./tools/probe/mv_probe_T 256 \
+          > $O/raw_${k}_ks$ks.log 2>&1 || exit 61
+      done
     done
-    grep -h "trace kind\|chunk  0\|workgroup end" $O/trace_*.log ;;
+    cat $O/raw_*.log | grep -v "^exp check" ;;
   diag04)
     # the round-4 library (lib/r04diag, built from commit 7eefa8d + the maps dump) under the
     # kernel trace that crashed in round 4
