@@ -511,51 +511,54 @@ hipError_t go(const CuParams & P, hipStream_t s) {
 
 
 // ---------------------------------------------------------------------------------------------
-// K-split decode matvec (k_mv_ks): the per-wave chain, not the weight stream, sets the time of a
-// decode matvec whose CU owns only a few row groups (7B Wo / W2: 2 groups per CU, one wave each
-// running 128 / 344 blocks in order, ~28 cycles per block; tools/probe traces).  Only the fp32
-// FMA of each block is serial in the reference's chain (acc_j = fmaf(s_b, P_bj, acc_j) in block
-// order, ggml.c:2013); the integer partials P_bj and the scale products s_b are not.  So each row
-// group is cut into S segments of consecutive 8-block sub-chunks, one wave per segment: every wave
-// loads its segment's weights, computes its P (v_dot8, exact integers |P| <= 256 kept as f16) and s
-// (= dw * dx, f32) into registers while the others do the same, and then the segments' FMAs run
-// in order as a baton: wave k waits for wave k-1's 64 chain values in LDS, continues the chains
-// with v_fma_mix (f32 s, f16 P: fmaf(s, (float) P, acc), one rounding), and hands them on.  The
-// last segment's wave reduces (AVX2 horizontal order) and runs the epilogue.  Bit-identical to
-// k_mv_cu by construction: the same FMAs in the same order.
-template <int S, int GMAX, int PRO, int EPI, int KT>
-__global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
-    constexpr int NW = S * GMAX;
+// Producer / consumer decode matvec (k_mv_pc) for the shapes whose CU owns only a few row groups
+// (7B Wo / W2: 2 per CU).  k_mv_cu runs each row group on ONE wave, ~34 cycles per block
+// (tools/probe traces, profiles/r05/raw_*), while the only serial part of the reference's chain
+// is its fp32 FMA (acc_j = fmaf(s_b, P_bj, acc_j) in block order, ggml.c:2013), ~8.7 cycles per
+// dependent step on this chip (tools/probe/chain_lat).  Here every row group has one CONSUMER
+// wave that only runs those FMAs, and P PRODUCER waves that stream the weights and turn each
+// 32-block chunk into the consumer's operands in an LDS ring: the integer partials P_bj (exact,
+// |P| <= 256, stored as f16) and the scale products s = dw * dx (f32, per row).  The consumer
+// continues the chains with v_fma_mix (f32 s, f16 P: fmaf(s, (float) P, acc), one rounding),
+// chunk after chunk in order, then reduces (AVX2 horizontal order) and runs the epilogue:
+// bit-identical to k_mv_cu by construction.  Ring hand-offs are LDS words (tags = chunk + 1).
+constexpr int PC_PSTRIDE = 80;                        // bytes per lane of a slot's P area (conflict-free b128)
+constexpr int PC_SLOT = 64 * PC_PSTRIDE + SPL * 4;    // P [64 lanes][32 f16] (padded) + s [8 rows][SRS]
+
+template <int GMAX, int NPR, int R, int PRO, int EPI, int KT>
+__global__ __launch_bounds__(GMAX * (1 + NPR) * 64) void k_mv_pc(CuParams P) {
+    constexpr int NW = GMAX * (1 + NPR);
     constexpr int NT = NW * 64;
     constexpr int nb = KT / 32;
-    constexpr int nsub = nb / 8;                 // 8-block sub-chunks of a row
+    constexpr int nsub = nb / 8;
     constexpr int NC = (nb + 31) / 32;
-    constexpr int SEG = (nsub + S - 1) / S;      // sub-chunks per segment (at most)
-    constexpr int SC = SEG / 4 + 2;              // chunks a segment can touch
     constexpr int nunits = KT / 8;
     constexpr bool FPRO = (PRO == PRO_NORM || PRO == PRO_ACTF);
+    constexpr int CPP = (NC + NPR - 1) / NPR;          // chunks per producer (at most)
     static_assert(nb % 8 == 0, "K must be a multiple of 256");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t * act = (uint32_t *) smem;                          // nb * 32 B
     float * dxp = (float *) (smem + nb * 32);                    // NC * 128 B
-    float * sbuf = dxp + NC * 32;                                // NW * SPL floats (one table per wave)
-    float * bacc = sbuf + NW * SPL;                              // GMAX * 64 chain values (the baton)
-    unsigned * bflag = (unsigned *) (bacc + GMAX * 64);          // GMAX baton words
-    double * red = (double *) (bflag + GMAX + (GMAX & 1));       // NW doubles
+    uint8_t * ring = (uint8_t *) (dxp + NC * 32);                // GMAX * R slots
+    unsigned * full = (unsigned *) (ring + (size_t) GMAX * R * PC_SLOT);   // [GMAX][R]
+    unsigned * freed = full + GMAX * R;                                     // [GMAX][R]
+    double * red = (double *) (freed + GMAX * R + ((GMAX * R) & 1));       // NW doubles
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int j = lane & 7, r = lane >> 3;
     LVK_T(0);
-    const int gi = wave / S, seg = wave - gi * S;              // this wave's row group and segment
+    // consumers are waves 0..GMAX-1 (one per SIMD while GMAX <= 4), then the producers
+    const bool consumer = wave < GMAX;
+    const int gi = consumer ? wave : (wave - GMAX) / NPR;
+    const int pk = consumer ? 0 : (wave - GMAX) - gi * NPR;
     const int g0 = (int) ((unsigned) blockIdx.x * (unsigned) P.G / (unsigned) gridDim.x);
     const int g1 = (int) ((unsigned) (blockIdx.x + 1) * (unsigned) P.G / (unsigned) gridDim.x);
     const bool has = g0 + gi < g1;
     const int grp = min(g0 + gi, P.G - 1);
-    const int u0 = seg * nsub / S, u1 = (seg + 1) * nsub / S;  // sub-chunks [u0, u1)
-    const int c0 = u0 >> 2;                                    // first chunk touched
+    uint8_t * gring = ring + (size_t) gi * R * PC_SLOT;
 
-    // 1. the prologue inputs, then this segment's weights and scales, all in flight at once
+    // 1. the prologue inputs, then (producers) the first chunk's weights
     constexpr int UM = FPRO ? (nunits + NT - 1) / NT : (nb + NT - 1) / NT;
     float4 xv[UM][2];
     float4 gv[PRO == PRO_NORM ? UM : 1][2];
@@ -580,19 +583,23 @@ __global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
             dv[k] = P.xq.d[b];
         }
     }
-    const uint32_t loff = has ? (uint32_t) lane * 16u : 0u;
-    uint4 W[SEG];
-    float4 SS[SC];
+    // producer weight registers: two chunk sets (the next chunk's loads go out before this one's work)
+    const uint32_t loff = (has && !consumer) ? (uint32_t) lane * 16u : 0u;
+    uint4 W[2][4];
+    float4 SW[2];
+    auto issue = [&](int set, int c) __attribute__((always_inline)) {
+        const int cc = min(c, NC - 1);
+        SW[set] = *(const float4 *) ((const char *) (P.scl + ((size_t) grp * NC + cc) * 64) + loff);
 #pragma unroll
-    for (int i = 0; i < SC; ++i) {
-        const int c = min(c0 + i, NC - 1);
-        SS[i] = *(const float4 *) ((const char *) (P.scl + ((size_t) grp * NC + c) * 64) + loff);
-    }
-#pragma unroll
-    for (int i = 0; i < SEG; ++i) {
-        const int u = min(u0 + i, nsub - 1);
-        W[i] = ld_nt((const uint4 *) ((const char *) (P.nib + ((size_t) grp * NC * 4 + u) * 64) + loff));
-    }
+        for (int sb = 0; sb < 4; ++sb) {
+            // (the zero-padded tail of a partial last chunk is never streamed: its slots re-read
+            // the last real sub-chunk, whose partials the consumer skips)
+            const int su = min(cc * 4 + sb, nsub - 1);
+            W[set][sb] = ld_nt((const uint4 *) ((const char *) (P.nib + ((size_t) grp * NC * 4 + su) * 64) + loff));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    if (!consumer) issue(0, pk);
 #pragma unroll
     for (int k = 0; k < UM; ++k) {
         if constexpr (FPRO) {
@@ -602,7 +609,7 @@ __global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
             launder(qv[k]); launder(dv[k]);
         }
     }
-    if (tid < GMAX) bflag[tid] = 0u;
+    if (tid < 2 * GMAX * R) full[tid] = 0u;     // full and freed are adjacent
     LVK_T(1);
 
     // 2. the activation table (every wave builds its share; matvec_common.h layout)
@@ -667,79 +674,96 @@ __global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
             }
         }
     }
-    __syncthreads();            // activation table and baton words ready
+    __syncthreads();            // activation table and ring words ready
     LVK_T(2);
     if (!has) return;
+    auto lds_u32 = [](const unsigned * p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    auto wait_tag = [&](const unsigned * p, unsigned want) __attribute__((always_inline)) {
+        // every wave of the workgroup is resident: the tag arrives; bounded all the same
+        for (int spins = 0; lds_u32(p) < want && spins < (1 << 22); ++spins) __builtin_amdgcn_s_sleep(1);
+    };
 
-    // 3. this segment's partials P (f16 pairs) and scale products s, chunk by chunk
-    uint32_t PH[SEG * 4];        // P of blocks 8i + 2t, 8i + 2t + 1 (halves) for sub-chunk i
-    float SV[SEG * 8];           // s of block 8i + t
-    float * sw = sbuf + wave * SPL;
-#pragma unroll
-    for (int i = 0; i < SEG; ++i) {
-        const int u = u0 + i;
-        if (u < u1) {
-            const int c = u >> 2;
-            if (i == 0 || (u & 3) == 0) {
-                // the scale table of chunk c: s = dw * dx of blocks 32c + 8m + j (ggml.c:1968)
+    if (!consumer) {
+        // ---- producer pk of row group gi: chunks pk, pk + NPR, ... (two register sets, the
+        // loop unrolled by two so that every set index is a compile-time constant)
+        auto chunk = [&](auto set_c, int i) __attribute__((always_inline)) {
+            constexpr int set = decltype(set_c)::value;
+            const int c = pk + i * NPR;
+            if (c + NPR < NC) issue(set ^ 1, c + NPR);
+            const int slot = c % R;
+            uint8_t * sl = gring + (size_t) slot * PC_SLOT;
+            if (c >= R) wait_tag(freed + gi * R + slot, (unsigned) (c - R + 1));
+            // s = dw * dx of blocks 32c + 8m + j (ggml.c:1968), row-major table [r][SRS]
+            {
                 const float4 dx = *(const float4 *) (dxp + c * 32 + j * 4);
-                const int ci = c - c0;             // (selects, not a dynamic register index)
-                float4 dw = SS[0];
-#pragma unroll
-                for (int k = 1; k < SC; ++k) if (ci == k) dw = SS[k];
-                *(float4 *) (sw + r * SRS + j * 4) = make_float4(dw.x * dx.x, dw.y * dx.y, dw.z * dx.z, dw.w * dx.w);
-                __builtin_amdgcn_wave_barrier();
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const float4 dw = SW[set];
+                *(float4 *) ((float *) (sl + 64 * PC_PSTRIDE) + r * SRS + j * 4) =
+                    make_float4(dw.x * dx.x, dw.y * dx.y, dw.z * dx.z, dw.w * dx.w);
             }
-            // blocks 8 (u & 3) + t of chunk c: table slot 4 t' + m with block 8m + t'
-            const int sb = u & 3;
+            // P of the chunk's blocks, as f16 pairs: dword q of the lane = blocks 2q, 2q + 1
+            uint32_t ph[16];
 #pragma unroll
-            for (int t = 0; t < 8; ++t) SV[i * 8 + t] = sw[r * SRS + t * 4 + sb];
-            const uint32_t wd[4] = {W[i].x, W[i].y, W[i].z, W[i].w};
+            for (int sb = 0; sb < 4; ++sb) {
+                const uint32_t wd[4] = {W[set][sb].x, W[set][sb].y, W[set][sb].z, W[set][sb].w};
 #pragma unroll
-            for (int pp = 0; pp < 2; ++pp) {
-                const uint4 a = *(const uint4 *) (act + ((size_t) (u * 2 + pp) * 8 + j) * 4);
-                const int p0 = dot8(wd[2 * pp], a.x), p1 = dot8(wd[2 * pp], a.y);
-                const int p2 = dot8(wd[2 * pp + 1], a.z), p3 = dot8(wd[2 * pp + 1], a.w);
-                PH[i * 4 + pp * 2] = (uint32_t) f16_bits_i(p0) | ((uint32_t) f16_bits_i(p1) << 16);
-                PH[i * 4 + pp * 2 + 1] = (uint32_t) f16_bits_i(p2) | ((uint32_t) f16_bits_i(p3) << 16);
+                for (int pp = 0; pp < 2; ++pp) {
+                    const int u4 = c * 8 + sb * 2 + pp;
+                    const uint4 a = *(const uint4 *) (act + ((size_t) min(u4, nb / 4 - 1) * 8 + j) * 4);
+                    const float f0 = (float) dot8(wd[2 * pp], a.x), f1 = (float) dot8(wd[2 * pp], a.y);
+                    const float f2 = (float) dot8(wd[2 * pp + 1], a.z), f3 = (float) dot8(wd[2 * pp + 1], a.w);
+                    ph[sb * 4 + pp * 2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(f0, f1));
+                    ph[sb * 4 + pp * 2 + 1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(f2, f3));
+                }
             }
-            if ((u & 3) == 3) __builtin_amdgcn_wave_barrier();   // the table is rewritten next chunk
-        }
-    }
-    LVK_T(3);
-
-    // 4. the baton: segment seg continues the chains of segment seg - 1
-    float acc = 0.0f;
-    if (seg > 0) {
-        unsigned * fl = bflag + gi;
-        bool ok = true;
-        for (int spins = 0; __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (unsigned) seg; ++spins) {
-            if (spins > (1 << 22)) { ok = false; break; }    // never expected: poison the rows
-            __builtin_amdgcn_s_sleep(1);
-        }
-        acc = ok ? bacc[gi * 64 + lane] : __builtin_nanf("");
-    }
-    LVK_T(4);
+            uint4 * pd = (uint4 *) (sl + lane * PC_PSTRIDE);
 #pragma unroll
-    for (int i = 0; i < SEG; ++i) {
-        if (u0 + i < u1) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                acc = fma_mix_f32_f16<0>(SV[i * 8 + 2 * t], PH[i * 4 + t], acc);
-                acc = fma_mix_f32_f16<1>(SV[i * 8 + 2 * t + 1], PH[i * 4 + t], acc);
-            }
+            for (int q = 0; q < 4; ++q) pd[q] = make_uint4(ph[4 * q], ph[4 * q + 1], ph[4 * q + 2], ph[4 * q + 3]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(full + gi * R + slot, (unsigned) (c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
+#pragma unroll 1
+        for (int i = 0; i < CPP; i += 2) {
+            if (pk + i * NPR >= NC) break;
+            chunk(std::integral_constant<int, 0>{}, i);
+            if (pk + (i + 1) * NPR >= NC) break;
+            chunk(std::integral_constant<int, 1>{}, i + 1);
         }
-    }
-    if (seg + 1 < S) {
-        LVK_T(5);
-        bacc[gi * 64 + lane] = acc;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(bflag + gi, (unsigned) (seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return;
     }
+
+    // ---- consumer of row group gi: the chains, chunk after chunk
+    LVK_T(3);
+    float acc = 0.0f;
+#pragma unroll 1
+    for (int c = 0; c < NC; ++c) {
+        const int slot = c % R;
+        const uint8_t * sl = gring + (size_t) slot * PC_SLOT;
+        wait_tag(full + gi * R + slot, (unsigned) (c + 1));
+        uint4 pq[4];
+        float sa[8][4];
+        const uint4 * ps = (const uint4 *) (sl + lane * PC_PSTRIDE);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pq[q] = ps[q];
+        const float * st = (const float *) (sl + 64 * PC_PSTRIDE) + r * SRS;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const float4 v = *(const float4 *) (st + jj * 4);
+            sa[jj][0] = v.x; sa[jj][1] = v.y; sa[jj][2] = v.z; sa[jj][3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(freed + gi * R + slot, (unsigned) (c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t ph[16] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w,
+                                 pq[2].x, pq[2].y, pq[2].z, pq[2].w, pq[3].x, pq[3].y, pq[3].z, pq[3].w};
+#pragma unroll
+        for (int b = 0; b < 32; b += 2) {
+            if (c * 32 + b < nb) {     // (nb % 8 == 0: whole pairs)
+                acc = fma_mix_f32_f16<0>(sa[b & 7][b >> 3], ph[b >> 1], acc);
+                acc = fma_mix_f32_f16<1>(sa[(b + 1) & 7][(b + 1) >> 3], ph[b >> 1], acc);
+            }
+        }
+    }
+    LVK_T(4);
     const float res = octet_reduce(acc);
-    LVK_T(5);
     const int row = grp * 8 + r;
     if constexpr (EPI == EPI_STORE) {
         if (j == 0) P.y[row] = res;
@@ -757,19 +781,20 @@ __global__ __launch_bounds__(S * GMAX * 64) void k_mv_ks(CuParams P) {
     }
 }
 
-template <int S, int GMAX, int PRO, int EPI, int KT>
-hipError_t go_ks(const CuParams & P, hipStream_t s) {
-    constexpr int nb = KT / 32, NC = (nb + 31) / 32, NW = S * GMAX;
+template <int GMAX, int NPR, int R, int PRO, int EPI, int KT>
+hipError_t go_pc(const CuParams & P, hipStream_t s) {
+    constexpr int nb = KT / 32, NC = (nb + 31) / 32, NW = GMAX * (1 + NPR);
     const int nwg = std::min(cu_count(), P.G);
     if ((P.G + nwg - 1) / nwg > GMAX) return hipErrorNotSupported;
-    const size_t lds = (size_t) nb * 32 + NC * 128 + (size_t) NW * SPL * 4 + GMAX * 64 * 4 + (GMAX + (GMAX & 1)) * 4 + NW * 8;
-    LVK_LAUNCH((k_mv_ks<S, GMAX, PRO, EPI, KT>), dim3(nwg), dim3(NW * 64), lds, s, P);
+    const size_t lds = (size_t) nb * 32 + NC * 128 + (size_t) GMAX * R * PC_SLOT + (2 * GMAX * R + 1) * 4 + 8 + NW * 8;
+    if (lds > 160 * 1024) return hipErrorNotSupported;
+    LVK_LAUNCH((k_mv_pc<GMAX, NPR, R, PRO, EPI, KT>), dim3(nwg), dim3(NW * 64), lds, s, P);
     return hipGetLastError();
 }
 
-// LVK_MV_KS=0 keeps the one-wave-per-row-group kernel for every shape (A/B)
-static bool ks_env() {
-    static const bool v = [] { const char * e = getenv("LVK_MV_KS"); return !e || atoi(e) != 0; }();
+// LVK_MV_PC=0 keeps one wave per row group for every shape (A/B)
+static bool pc_env() {
+    static const bool v = [] { const char * e = getenv("LVK_MV_PC"); return !e || atoi(e) != 0; }();
     return v;
 }
 }  // namespace
@@ -851,8 +876,8 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
             case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 4096, 1>(P, s); break;
             case EPI_RESID:
                 if (pro == PRO_ACTQ) {
-                    if (ks_env()) {
-                        const hipError_t e = go_ks<4, 2, PRO_ACTQ, EPI_RESID, 4096>(P, s);
+                    if (pc_env()) {
+                        const hipError_t e = go_pc<2, 3, 4, PRO_ACTQ, EPI_RESID, 4096>(P, s);
                         if (e != hipErrorNotSupported) return e;
                     }
                     return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096, 5>(P, s);
@@ -877,8 +902,8 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         // profiles/r03_np_sweep.txt: 7.0 us against 8.6-9.3 for 8 waves that all quantize u
         // and then issue the weights)
         if (epi == EPI_RESID && pro == PRO_ACTF) {
-            if (ks_env()) {
-                const hipError_t e = go_ks<6, 2, PRO_ACTF, EPI_RESID, 11008>(P, s);
+            if (pc_env()) {
+                const hipError_t e = go_pc<2, 3, 4, PRO_ACTF, EPI_RESID, 11008>(P, s);
                 if (e != hipErrorNotSupported) return e;
             }
             // (needs at most 2 row groups per CU: a device with fewer CUs takes 8 waves that

@@ -51,6 +51,23 @@ for step in "$@"; do
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
       python3 tools/decode_speed.py 65b 16 > $O/kt65.log 2>&1 || exit 32
     find $O -name '*kernel_stats.csv' ;;
+  pc)
+    # the producer / consumer decode matvec (Wo, W2): parity of the 7B-shaped / full 7B decode, then
+    # A/B speed and per-wave phase stamps
+    O=gpurun_out/r05_pc; mkdir -p $O
+    timeout -k 10 900 $T tests/test_gpu_model.py tests/test_gpu_decode_chain.py tests/test_gpu_7b_full.py \
+      > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 51; }
+    tail -2 $O/tests.log
+    for r in 1 2; do
+      for k in 0 1; do
+        LVK_MV_PC=$k timeout -k 10 300 python3 tools/decode_speed.py 7b 96 2>/dev/null \
+          | sed "s/^{/{\"pc\": $k, /" | tee -a $O/ab.jsonl || exit 52
+      done
+    done
+    for k in 2 4; do
+      LVK_TRACE_RAW=1 LVK_TRACE_KIND=$k timeout -k 10 120 ./tools/probe/mv_probe_T 256 > $O/raw_${k}.log 2>&1 || exit 53
+    done
+    cat $O/raw_*.log | grep -v "^exp check" ;;
   ks)
     # the K-split decode matvec (Wo, W2): parity of the 7B-shaped / full 7B decode, then A/B speed
     O=gpurun_out/r05_ks; mkdir -p $O
