@@ -583,23 +583,27 @@ __global__ __launch_bounds__(GMAX * (1 + NPR) * 64) void k_mv_pc(CuParams P) {
             dv[k] = P.xq.d[b];
         }
     }
-    // producer weight registers: two chunk sets (the next chunk's loads go out before this one's work)
+    // producer weights: the first chunk of every producer goes out with the prologue inputs, the
+    // rest right after the table barrier (a CU's issue is throttled once its memory queue is full:
+    // issuing everything first would hold the table -- and every chain -- back; matvec rule 9).
+    // Consumer waves issue the same loads with every lane on one word, so no branch separates
+    // the issue from the waits (hipcc merges a branch join's wait counts conservatively: rule 8).
     const uint32_t loff = (has && !consumer) ? (uint32_t) lane * 16u : 0u;
-    uint4 W[2][4];
-    float4 SW[2];
-    auto issue = [&](int set, int c) __attribute__((always_inline)) {
-        const int cc = min(c, NC - 1);
-        SW[set] = *(const float4 *) ((const char *) (P.scl + ((size_t) grp * NC + cc) * 64) + loff);
+    uint4 W[CPP][4];
+    float4 SW[CPP];
+    auto issue = [&](const int i) __attribute__((always_inline)) {
+        const int cc = min(pk + i * NPR, NC - 1);
+        SW[i] = *(const float4 *) ((const char *) (P.scl + ((size_t) grp * NC + cc) * 64) + loff);
 #pragma unroll
         for (int sb = 0; sb < 4; ++sb) {
             // (the zero-padded tail of a partial last chunk is never streamed: its slots re-read
             // the last real sub-chunk, whose partials the consumer skips)
             const int su = min(cc * 4 + sb, nsub - 1);
-            W[set][sb] = ld_nt((const uint4 *) ((const char *) (P.nib + ((size_t) grp * NC * 4 + su) * 64) + loff));
+            W[i][sb] = ld_nt((const uint4 *) ((const char *) (P.nib + ((size_t) grp * NC * 4 + su) * 64) + loff));
         }
         __builtin_amdgcn_sched_barrier(0);
     };
-    if (!consumer) issue(0, pk);
+    issue(0);
 #pragma unroll
     for (int k = 0; k < UM; ++k) {
         if constexpr (FPRO) {
@@ -677,6 +681,10 @@ __global__ __launch_bounds__(GMAX * (1 + NPR) * 64) void k_mv_pc(CuParams P) {
     __syncthreads();            // activation table and ring words ready
     LVK_T(2);
     if (!has) return;
+    if (!consumer) {
+#pragma unroll
+        for (int i = 1; i < CPP; ++i) issue(i);
+    }
     auto lds_u32 = [](const unsigned * p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     auto wait_tag = [&](const unsigned * p, unsigned want) __attribute__((always_inline)) {
         // every wave of the workgroup is resident: the tag arrives; bounded all the same
@@ -684,19 +692,23 @@ __global__ __launch_bounds__(GMAX * (1 + NPR) * 64) void k_mv_pc(CuParams P) {
     };
 
     if (!consumer) {
-        // ---- producer pk of row group gi: chunks pk, pk + NPR, ... (two register sets, the
-        // loop unrolled by two so that every set index is a compile-time constant)
-        auto chunk = [&](auto set_c, int i) __attribute__((always_inline)) {
-            constexpr int set = decltype(set_c)::value;
+        // ---- producer pk of row group gi: chunks pk, pk + NPR, ..., every one already in flight
+#pragma unroll
+        for (int i = 0; i < CPP; ++i) {
             const int c = pk + i * NPR;
-            if (c + NPR < NC) issue(set ^ 1, c + NPR);
+            if (c >= NC) break;
             const int slot = c % R;
             uint8_t * sl = gring + (size_t) slot * PC_SLOT;
             if (c >= R) wait_tag(freed + gi * R + slot, (unsigned) (c - R + 1));
-            // s = dw * dx of blocks 32c + 8m + j (ggml.c:1968), row-major table [r][SRS]
+            // the chunk's LDS operands in one round trip: dx of blocks 32c + 8m + j and the
+            // activation words of its 8 four-block groups
+            const float4 dx = *(const float4 *) (dxp + c * 32 + j * 4);
+            uint4 A[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) A[q] = *(const uint4 *) (act + ((size_t) min(c * 8 + q, nb / 4 - 1) * 8 + j) * 4);
+            // s = dw * dx (ggml.c:1968), row-major table [r][SRS]
             {
-                const float4 dx = *(const float4 *) (dxp + c * 32 + j * 4);
-                const float4 dw = SW[set];
+                const float4 dw = SW[i];
                 *(float4 *) ((float *) (sl + 64 * PC_PSTRIDE) + r * SRS + j * 4) =
                     make_float4(dw.x * dx.x, dw.y * dx.y, dw.z * dx.z, dw.w * dx.w);
             }
@@ -704,11 +716,10 @@ __global__ __launch_bounds__(GMAX * (1 + NPR) * 64) void k_mv_pc(CuParams P) {
             uint32_t ph[16];
 #pragma unroll
             for (int sb = 0; sb < 4; ++sb) {
-                const uint32_t wd[4] = {W[set][sb].x, W[set][sb].y, W[set][sb].z, W[set][sb].w};
+                const uint32_t wd[4] = {W[i][sb].x, W[i][sb].y, W[i][sb].z, W[i][sb].w};
 #pragma unroll
                 for (int pp = 0; pp < 2; ++pp) {
-                    const int u4 = c * 8 + sb * 2 + pp;
-                    const uint4 a = *(const uint4 *) (act + ((size_t) min(u4, nb / 4 - 1) * 8 + j) * 4);
+                    const uint4 a = A[sb * 2 + pp];
                     const float f0 = (float) dot8(wd[2 * pp], a.x), f1 = (float) dot8(wd[2 * pp], a.y);
                     const float f2 = (float) dot8(wd[2 * pp + 1], a.z), f3 = (float) dot8(wd[2 * pp + 1], a.w);
                     ph[sb * 4 + pp * 2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(f0, f1));
@@ -720,13 +731,7 @@ __global__ __launch_bounds__(GMAX * (1 + NPR) * 64) void k_mv_pc(CuParams P) {
             for (int q = 0; q < 4; ++q) pd[q] = make_uint4(ph[4 * q], ph[4 * q + 1], ph[4 * q + 2], ph[4 * q + 3]);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) __hip_atomic_store(full + gi * R + slot, (unsigned) (c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        };
-#pragma unroll 1
-        for (int i = 0; i < CPP; i += 2) {
-            if (pk + i * NPR >= NC) break;
-            chunk(std::integral_constant<int, 0>{}, i);
-            if (pk + (i + 1) * NPR >= NC) break;
-            chunk(std::integral_constant<int, 1>{}, i + 1);
+            LVK_T(8 + i);
         }
         return;
     }
@@ -739,6 +744,7 @@ __global__ __launch_bounds__(GMAX * (1 + NPR) * 64) void k_mv_pc(CuParams P) {
         const int slot = c % R;
         const uint8_t * sl = gring + (size_t) slot * PC_SLOT;
         wait_tag(full + gi * R + slot, (unsigned) (c + 1));
+        LVK_T(8 + c);
         uint4 pq[4];
         float sa[8][4];
         const uint4 * ps = (const uint4 *) (sl + lane * PC_PSTRIDE);
@@ -792,9 +798,9 @@ hipError_t go_pc(const CuParams & P, hipStream_t s) {
     return hipGetLastError();
 }
 
-// LVK_MV_PC=0 keeps one wave per row group for every shape (A/B)
-static bool pc_env() {
-    static const bool v = [] { const char * e = getenv("LVK_MV_PC"); return !e || atoi(e) != 0; }();
+// LVK_MV_PC=0 keeps one wave per row group for every shape; 1 / 2: 3 / 5 producers per group (A/B)
+static int pc_env() {
+    static const int v = [] { const char * e = getenv("LVK_MV_PC"); return e ? atoi(e) : 1; }();
     return v;
 }
 }  // namespace
@@ -877,7 +883,8 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
             case EPI_RESID:
                 if (pro == PRO_ACTQ) {
                     if (pc_env()) {
-                        const hipError_t e = go_pc<2, 3, 4, PRO_ACTQ, EPI_RESID, 4096>(P, s);
+                        const hipError_t e = pc_env() == 2 ? go_pc<2, 5, 4, PRO_ACTQ, EPI_RESID, 4096>(P, s)
+                                                           : go_pc<2, 3, 4, PRO_ACTQ, EPI_RESID, 4096>(P, s);
                         if (e != hipErrorNotSupported) return e;
                     }
                     return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096, 5>(P, s);
@@ -903,7 +910,8 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         // and then issue the weights)
         if (epi == EPI_RESID && pro == PRO_ACTF) {
             if (pc_env()) {
-                const hipError_t e = go_pc<2, 3, 4, PRO_ACTF, EPI_RESID, 11008>(P, s);
+                const hipError_t e = pc_env() == 2 ? go_pc<2, 5, 4, PRO_ACTF, EPI_RESID, 11008>(P, s)
+                                                   : go_pc<2, 3, 4, PRO_ACTF, EPI_RESID, 11008>(P, s);
                 if (e != hipErrorNotSupported) return e;
             }
             // (needs at most 2 row groups per CU: a device with fewer CUs takes 8 waves that

@@ -59,13 +59,15 @@ for step in "$@"; do
       > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 51; }
     tail -2 $O/tests.log
     for r in 1 2; do
-      for k in 0 1; do
+      for k in 0 1 2; do
         LVK_MV_PC=$k timeout -k 10 300 python3 tools/decode_speed.py 7b 96 2>/dev/null \
           | sed "s/^{/{\"pc\": $k, /" | tee -a $O/ab.jsonl || exit 52
       done
     done
     for k in 2 4; do
-      LVK_TRACE_RAW=1 LVK_TRACE_KIND=$k timeout -k 10 120 ./tools/probe/mv_probe_T 256 > $O/raw_${k}.log 2>&1 || exit 53
+      for v in 1 2; do
+        LVK_MV_PC=$v LVK_TRACE_RAW=1 LVK_TRACE_KIND=$k timeout -k 10 120 ./tools/probe/mv_probe_T 256 > $O/raw_${k}_pc$v.log 2>&1 || exit 53
+      done
     done
     cat $O/raw_*.log | grep -v "^exp check" ;;
   ks)

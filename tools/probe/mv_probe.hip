@@ -274,16 +274,16 @@ int main(int argc, char ** argv) {
             for (int w = 0; w < 256 * 16; w++) if (h[(size_t) w * 64]) { t0 = std::min(t0, h[(size_t) w * 64]); }
             printf("raw trace kind %s (cycles after the wave's entry; entry after the first wave's entry):\n", names[kind]);
             for (int wi = 0; wi < 16; wi++) {
-                double a[8] = {0}; int c[8] = {0}; int nw = 0; double ent = 0;
+                double a[40] = {0}; int c[40] = {0}; int nw = 0; double ent = 0;
                 for (int b = 0; b < 256; b++) {
                     unsigned long long * e = &h[((size_t) b * 16 + wi) * 64];
                     if (!e[0]) continue;
                     nw++; ent += (double) (e[0] - t0);
-                    for (int k = 1; k < 8; k++) if (e[k]) { a[k] += (double) (e[k] - e[0]); c[k]++; tend = std::max(tend, e[k]); }
+                    for (int k = 1; k < 40; k++) if (e[k]) { a[k] += (double) (e[k] - e[0]); c[k]++; tend = std::max(tend, e[k]); }
                 }
                 if (!nw) continue;
                 printf("  wave %2d (%3d wgs) entry %6.0f:", wi, nw, ent / nw);
-                for (int k = 1; k < 8; k++) if (c[k]) printf("  e%d %6.0f", k, a[k] / c[k]);
+                for (int k = 1; k < 40; k++) if (c[k]) printf(" e%d %.0f", k, a[k] / c[k]);
                 printf("\n");
             }
             printf("  first entry -> last stamp %llu cycles\n", tend - t0);
