@@ -205,21 +205,4 @@ __device__ __forceinline__ float fma_mix_hh(uint32_t a, uint32_t b, float c) {
     return d;
 }
 
-// f16 bits of a small integer (|v| <= 2048: exact), v_cvt_f16_i16
-__device__ __forceinline__ uint16_t f16_bits_i(int v) {
-    uint32_t r;
-    asm volatile("v_cvt_f16_i16 %0, %1" : "=v"(r) : "v"(v));
-    return (uint16_t) r;
-}
-// fmaf(s, (float) f16 half H of p, c): v_fma_mix converts the f16 operand exactly, one rounding
-template <int H>
-__device__ __forceinline__ float fma_mix_f32_f16(float s, uint32_t p, float c) {
-    float d;
-    if constexpr (H == 0)
-        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(s), "v"(p), "v"(c));
-    else
-        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(s), "v"(p), "v"(c));
-    return d;
-}
-
 }  // namespace lvk

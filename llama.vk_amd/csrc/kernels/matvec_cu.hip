@@ -509,300 +509,6 @@ hipError_t go(const CuParams & P, hipStream_t s) {
     return hipGetLastError();
 }
 
-
-// ---------------------------------------------------------------------------------------------
-// Producer / consumer decode matvec (k_mv_pc) for the shapes whose CU owns only a few row groups
-// (7B Wo / W2: 2 per CU).  k_mv_cu runs each row group on ONE wave, ~34 cycles per block
-// (tools/probe traces, profiles/r05/raw_*), while the only serial part of the reference's chain
-// is its fp32 FMA (acc_j = fmaf(s_b, P_bj, acc_j) in block order, ggml.c:2013), ~8.7 cycles per
-// dependent step on this chip (tools/probe/chain_lat).  Here every row group has one CONSUMER
-// wave that only runs those FMAs, and P PRODUCER waves that stream the weights and turn each
-// 32-block chunk into the consumer's operands in an LDS ring: the integer partials P_bj (exact,
-// |P| <= 256, stored as f16) and the scale products s = dw * dx (f32, per row).  The consumer
-// continues the chains with v_fma_mix (f32 s, f16 P: fmaf(s, (float) P, acc), one rounding),
-// chunk after chunk in order, then reduces (AVX2 horizontal order) and runs the epilogue:
-// bit-identical to k_mv_cu by construction.  Ring hand-offs are LDS words (tags = chunk + 1).
-constexpr int PC_PSTRIDE = 80;                        // bytes per lane of a slot's P area (conflict-free b128)
-constexpr int PC_SLOT = 64 * PC_PSTRIDE + SPL * 4;    // P [64 lanes][32 f16] (padded) + s [8 rows][SRS]
-
-template <int GMAX, int NPR, int R, int PRO, int EPI, int KT>
-__global__ __launch_bounds__(GMAX * (1 + NPR) * 64) void k_mv_pc(CuParams P) {
-    constexpr int NW = GMAX * (1 + NPR);
-    constexpr int NT = NW * 64;
-    constexpr int nb = KT / 32;
-    constexpr int nsub = nb / 8;
-    constexpr int NC = (nb + 31) / 32;
-    constexpr int nunits = KT / 8;
-    constexpr bool FPRO = (PRO == PRO_NORM || PRO == PRO_ACTF);
-    constexpr int CPP = (NC + NPR - 1) / NPR;          // chunks per producer (at most)
-    static_assert(nb % 8 == 0, "K must be a multiple of 256");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t * act = (uint32_t *) smem;                          // nb * 32 B
-    float * dxp = (float *) (smem + nb * 32);                    // NC * 128 B
-    uint8_t * ring = (uint8_t *) (dxp + NC * 32);                // GMAX * R slots
-    unsigned * full = (unsigned *) (ring + (size_t) GMAX * R * PC_SLOT);   // [GMAX][R]
-    unsigned * freed = full + GMAX * R;                                     // [GMAX][R]
-    double * red = (double *) (freed + GMAX * R + ((GMAX * R) & 1));       // NW doubles
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int j = lane & 7, r = lane >> 3;
-    LVK_T(0);
-    // consumers are waves 0..GMAX-1 (one per SIMD while GMAX <= 4), then the producers
-    const bool consumer = wave < GMAX;
-    const int gi = consumer ? wave : (wave - GMAX) / NPR;
-    const int pk = consumer ? 0 : (wave - GMAX) - gi * NPR;
-    const int g0 = (int) ((unsigned) blockIdx.x * (unsigned) P.G / (unsigned) gridDim.x);
-    const int g1 = (int) ((unsigned) (blockIdx.x + 1) * (unsigned) P.G / (unsigned) gridDim.x);
-    const bool has = g0 + gi < g1;
-    const int grp = min(g0 + gi, P.G - 1);
-    uint8_t * gring = ring + (size_t) gi * R * PC_SLOT;
-
-    // 1. the prologue inputs, then (producers) the first chunk's weights
-    constexpr int UM = FPRO ? (nunits + NT - 1) / NT : (nb + NT - 1) / NT;
-    float4 xv[UM][2];
-    float4 gv[PRO == PRO_NORM ? UM : 1][2];
-    uint4 qv[FPRO ? 1 : UM];
-    float dv[FPRO ? 1 : UM];
-    if constexpr (FPRO) {
-#pragma unroll
-        for (int k = 0; k < UM; ++k) {
-            const int un = min(k * NT + tid, nunits - 1);
-            const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
-            xv[k][0] = xp[0]; xv[k][1] = xp[1];
-            if constexpr (PRO == PRO_NORM) {
-                const float4 * gp = (const float4 *) (P.g + (size_t) un * 8);
-                gv[k][0] = gp[0]; gv[k][1] = gp[1];
-            }
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < UM; ++k) {
-            const int b = min(k * NT + tid, nb - 1);
-            qv[k] = P.xq.qs[b];
-            dv[k] = P.xq.d[b];
-        }
-    }
-    // producer weights: the first chunk of every producer goes out with the prologue inputs, the
-    // rest right after the table barrier (a CU's issue is throttled once its memory queue is full:
-    // issuing everything first would hold the table -- and every chain -- back; matvec rule 9).
-    // Consumer waves issue the same loads with every lane on one word, so no branch separates
-    // the issue from the waits (hipcc merges a branch join's wait counts conservatively: rule 8).
-    const uint32_t loff = (has && !consumer) ? (uint32_t) lane * 16u : 0u;
-    uint4 W[CPP][4];
-    float4 SW[CPP];
-    auto issue = [&](const int i) __attribute__((always_inline)) {
-        const int cc = min(pk + i * NPR, NC - 1);
-        SW[i] = *(const float4 *) ((const char *) (P.scl + ((size_t) grp * NC + cc) * 64) + loff);
-#pragma unroll
-        for (int sb = 0; sb < 4; ++sb) {
-            // (the zero-padded tail of a partial last chunk is never streamed: its slots re-read
-            // the last real sub-chunk, whose partials the consumer skips)
-            const int su = min(cc * 4 + sb, nsub - 1);
-            W[i][sb] = ld_nt((const uint4 *) ((const char *) (P.nib + ((size_t) grp * NC * 4 + su) * 64) + loff));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    issue(0);
-#pragma unroll
-    for (int k = 0; k < UM; ++k) {
-        if constexpr (FPRO) {
-            launder(xv[k][0]); launder(xv[k][1]);
-            if constexpr (PRO == PRO_NORM) { launder(gv[k][0]); launder(gv[k][1]); }
-        } else {
-            launder(qv[k]); launder(dv[k]);
-        }
-    }
-    if (tid < 2 * GMAX * R) full[tid] = 0u;     // full and freed are adjacent
-    LVK_T(1);
-
-    // 2. the activation table (every wave builds its share; matvec_common.h layout)
-    if constexpr (FPRO) {
-        float scale = 1.0f;
-        if constexpr (PRO == PRO_NORM) {
-            // ggml_compute_forward_rms_norm_f32 (ggml.c:6058-6076), as mv_cu_run
-            double acc = 0.0;
-#pragma unroll
-            for (int k = 0; k < UM; ++k) {
-                if (k * NT + tid < nunits) {
-                    const float e[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
-                                        xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) { const float sq = e[q] * e[q]; acc += (double) sq; }
-                }
-            }
-            acc = wave_sum_d(acc);
-            if (lane == 0) red[wave] = acc;
-            __syncthreads();
-            double sum = red[0];
-            for (int w = 1; w < NW; ++w) sum += red[w];
-            const float mean = (float) (sum / (double) KT);
-            scale = 1.0f / sqrtf(mean + 1e-6f);
-        }
-#pragma unroll
-        for (int k = 0; k < UM; ++k) {
-            if (k * NT >= nunits) break;
-            const int un = k * NT + tid;
-            float v[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
-                          xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
-            float amax = 0.0f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                if constexpr (PRO == PRO_NORM) {
-                    const float gg[8] = {gv[k][0].x, gv[k][0].y, gv[k][0].z, gv[k][0].w,
-                                         gv[k][1].x, gv[k][1].y, gv[k][1].z, gv[k][1].w};
-                    const float yn = v[e] * scale;      // ggml_vec_scale_f32 (ggml.c:6076)
-                    v[e] = gg[e] * yn;                  // ggml_mul(repeat(g), cur) (llama.cpp:984)
-                }
-                const float a = fabsf(v[e]);
-                amax = a > amax ? a : amax;
-            }
-            const float o0 = quad_bcast<0>(amax), o1 = quad_bcast<1>(amax);
-            const float o2 = quad_bcast<2>(amax), o3 = quad_bcast<3>(amax);
-            const float m01 = o1 > o0 ? o1 : o0, m23 = o3 > o2 ? o3 : o2;
-            amax = m23 > m01 ? m23 : m01;
-            const float d = amax / 7.0f;                              // ggml.c:651
-            const float id = (amax != 0.0f) ? 7.0f / amax : 0.0f;     // ggml.c:653
-            const uint32_t w = q40_pack8(v, id);
-            if (un < nunits) act_store(act, dxp, un >> 2, un & 3, w, d, (un & 3) == 0);
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < UM; ++k) {
-            const int b = k * NT + tid;
-            if (b < nb) {
-                act_store(act, dxp, b, 0, qv[k].x, dv[k], true);
-                act_store(act, dxp, b, 1, qv[k].y, 0.0f, false);
-                act_store(act, dxp, b, 2, qv[k].z, 0.0f, false);
-                act_store(act, dxp, b, 3, qv[k].w, 0.0f, false);
-            }
-        }
-    }
-    __syncthreads();            // activation table and ring words ready
-    LVK_T(2);
-    if (!has) return;
-    if (!consumer) {
-#pragma unroll
-        for (int i = 1; i < CPP; ++i) issue(i);
-    }
-    auto lds_u32 = [](const unsigned * p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-    auto wait_tag = [&](const unsigned * p, unsigned want) __attribute__((always_inline)) {
-        // every wave of the workgroup is resident: the tag arrives; bounded all the same
-        for (int spins = 0; lds_u32(p) < want && spins < (1 << 22); ++spins) __builtin_amdgcn_s_sleep(1);
-    };
-
-    if (!consumer) {
-        // ---- producer pk of row group gi: chunks pk, pk + NPR, ..., every one already in flight
-#pragma unroll
-        for (int i = 0; i < CPP; ++i) {
-            const int c = pk + i * NPR;
-            if (c >= NC) break;
-            const int slot = c % R;
-            uint8_t * sl = gring + (size_t) slot * PC_SLOT;
-            if (c >= R) wait_tag(freed + gi * R + slot, (unsigned) (c - R + 1));
-            // the chunk's LDS operands in one round trip: dx of blocks 32c + 8m + j and the
-            // activation words of its 8 four-block groups
-            const float4 dx = *(const float4 *) (dxp + c * 32 + j * 4);
-            uint4 A[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) A[q] = *(const uint4 *) (act + ((size_t) min(c * 8 + q, nb / 4 - 1) * 8 + j) * 4);
-            // s = dw * dx (ggml.c:1968), row-major table [r][SRS]
-            {
-                const float4 dw = SW[i];
-                *(float4 *) ((float *) (sl + 64 * PC_PSTRIDE) + r * SRS + j * 4) =
-                    make_float4(dw.x * dx.x, dw.y * dx.y, dw.z * dx.z, dw.w * dx.w);
-            }
-            // P of the chunk's blocks, as f16 pairs: dword q of the lane = blocks 2q, 2q + 1
-            uint32_t ph[16];
-#pragma unroll
-            for (int sb = 0; sb < 4; ++sb) {
-                const uint32_t wd[4] = {W[i][sb].x, W[i][sb].y, W[i][sb].z, W[i][sb].w};
-#pragma unroll
-                for (int pp = 0; pp < 2; ++pp) {
-                    const uint4 a = A[sb * 2 + pp];
-                    const float f0 = (float) dot8(wd[2 * pp], a.x), f1 = (float) dot8(wd[2 * pp], a.y);
-                    const float f2 = (float) dot8(wd[2 * pp + 1], a.z), f3 = (float) dot8(wd[2 * pp + 1], a.w);
-                    ph[sb * 4 + pp * 2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(f0, f1));
-                    ph[sb * 4 + pp * 2 + 1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(f2, f3));
-                }
-            }
-            uint4 * pd = (uint4 *) (sl + lane * PC_PSTRIDE);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) pd[q] = make_uint4(ph[4 * q], ph[4 * q + 1], ph[4 * q + 2], ph[4 * q + 3]);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_store(full + gi * R + slot, (unsigned) (c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            LVK_T(8 + i);
-        }
-        return;
-    }
-
-    // ---- consumer of row group gi: the chains, chunk after chunk
-    LVK_T(3);
-    float acc = 0.0f;
-#pragma unroll 1
-    for (int c = 0; c < NC; ++c) {
-        const int slot = c % R;
-        const uint8_t * sl = gring + (size_t) slot * PC_SLOT;
-        wait_tag(full + gi * R + slot, (unsigned) (c + 1));
-        LVK_T(8 + c);
-        uint4 pq[4];
-        float sa[8][4];
-        const uint4 * ps = (const uint4 *) (sl + lane * PC_PSTRIDE);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) pq[q] = ps[q];
-        const float * st = (const float *) (sl + 64 * PC_PSTRIDE) + r * SRS;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-            const float4 v = *(const float4 *) (st + jj * 4);
-            sa[jj][0] = v.x; sa[jj][1] = v.y; sa[jj][2] = v.z; sa[jj][3] = v.w;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(freed + gi * R + slot, (unsigned) (c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t ph[16] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w,
-                                 pq[2].x, pq[2].y, pq[2].z, pq[2].w, pq[3].x, pq[3].y, pq[3].z, pq[3].w};
-#pragma unroll
-        for (int b = 0; b < 32; b += 2) {
-            if (c * 32 + b < nb) {     // (nb % 8 == 0: whole pairs)
-                acc = fma_mix_f32_f16<0>(sa[b & 7][b >> 3], ph[b >> 1], acc);
-                acc = fma_mix_f32_f16<1>(sa[(b + 1) & 7][(b + 1) >> 3], ph[b >> 1], acc);
-            }
-        }
-    }
-    LVK_T(4);
-    const float res = octet_reduce(acc);
-    const int row = grp * 8 + r;
-    if constexpr (EPI == EPI_STORE) {
-        if (j == 0) P.y[row] = res;
-    } else if constexpr (EPI == EPI_RESID) {
-        if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
-    } else if constexpr (EPI == EPI_QKV) {
-        const StepParams * sp = P.sp;
-        qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32);
-    } else if constexpr (EPI == EPI_SWIGLU_F32) {
-        const float a3 = __shfl_xor(res, 32);
-        if (r < 4 && j == 0) {
-            const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res)]);   // ggml_vec_silu_f32 (ggml.c:2495)
-            P.u[grp * 4 + r] = sl * a3;                                  // ggml_mul (llama.cpp:1096)
-        }
-    }
-}
-
-template <int GMAX, int NPR, int R, int PRO, int EPI, int KT>
-hipError_t go_pc(const CuParams & P, hipStream_t s) {
-    constexpr int nb = KT / 32, NC = (nb + 31) / 32, NW = GMAX * (1 + NPR);
-    const int nwg = std::min(cu_count(), P.G);
-    if ((P.G + nwg - 1) / nwg > GMAX) return hipErrorNotSupported;
-    const size_t lds = (size_t) nb * 32 + NC * 128 + (size_t) GMAX * R * PC_SLOT + (2 * GMAX * R + 1) * 4 + 8 + NW * 8;
-    if (lds > 160 * 1024) return hipErrorNotSupported;
-    LVK_LAUNCH((k_mv_pc<GMAX, NPR, R, PRO, EPI, KT>), dim3(nwg), dim3(NW * 64), lds, s, P);
-    return hipGetLastError();
-}
-
-// LVK_MV_PC=0 keeps one wave per row group for every shape; 1 / 2: 3 / 5 producers per group (A/B)
-static int pc_env() {
-    static const int v = [] { const char * e = getenv("LVK_MV_PC"); return e ? atoi(e) : 1; }();
-    return v;
-}
 }  // namespace
 
 // CUs of the current device, cached per device id (a one-process layer split may drive
@@ -881,14 +587,7 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
             case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 4096, 5>(P, s); break;
             case EPI_STORE: if (pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 4096, 1>(P, s); break;
             case EPI_RESID:
-                if (pro == PRO_ACTQ) {
-                    if (pc_env()) {
-                        const hipError_t e = pc_env() == 2 ? go_pc<2, 5, 4, PRO_ACTQ, EPI_RESID, 4096>(P, s)
-                                                           : go_pc<2, 3, 4, PRO_ACTQ, EPI_RESID, 4096>(P, s);
-                        if (e != hipErrorNotSupported) return e;
-                    }
-                    return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096, 5>(P, s);
-                }
+                if (pro == PRO_ACTQ) return go<2, 0, 2, PRO_ACTQ, EPI_RESID, 4096, 5>(P, s);
                 break;
         }
         // operator API (lvk_mul_mat_q: plain quantize of an f32 input)
@@ -909,11 +608,6 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         // profiles/r03_np_sweep.txt: 7.0 us against 8.6-9.3 for 8 waves that all quantize u
         // and then issue the weights)
         if (epi == EPI_RESID && pro == PRO_ACTF) {
-            if (pc_env()) {
-                const hipError_t e = pc_env() == 2 ? go_pc<2, 5, 4, PRO_ACTF, EPI_RESID, 11008>(P, s)
-                                                   : go_pc<2, 3, 4, PRO_ACTF, EPI_RESID, 11008>(P, s);
-                if (e != hipErrorNotSupported) return e;
-            }
             // (needs at most 2 row groups per CU: a device with fewer CUs takes 8 waves that
             // all quantize u, then issue the weights)
             const hipError_t e = go<2, 6, 4, PRO_ACTF, EPI_RESID, 11008, 0>(P, s);

@@ -1,10 +1,16 @@
 # Round-5 GPU runs, one or more steps per call (gpurun -- bash tools/gpu_r05.sh STEP...); every GPU
 # step runs under its own time limit and the first failure ends the call.
 #   suite       the whole -m gpu test suite                          -> gpurun_out/gputests.log
+#   bench       bench.py at its defaults (N = 1)                      -> gpurun_out/r05_bench.json
+#   kt          kernel-trace summaries: 7B bench legs, 13B Q4_1 decode, 7B 512-token prompt
+#                                                                     -> gpurun_out/r05_kt/
+#   pmc         FETCH_SIZE / WRITE_SIZE per decode kernel, 7B and 13B -> gpurun_out/r05_traffic.json
+#   sq          SQ issue / wait counters per decode kernel (7B)       -> gpurun_out/r05_sq/sq_decode_7b.json
+#   split       65B layer split over 2 ranks on the one GPU through the shm stage link
+#                                                                     -> gpurun_out/r05_bench_split_shm_s2.json
 #   l2          L2 retention across launches (tools/probe/l2_probe)   -> gpurun_out/r05_l2/
-#   diag65      the 65B decode under rocprofv3 --kernel-trace with LVK_SEGV_TRACE=1 (native frames
-#               and /proc/self/maps on a fault)                      -> gpurun_out/r05_diag65/
-#   prof65      the same trace, expected to complete                 -> gpurun_out/r05_prof65/
+#   trace       per-wave phase stamps of the Wo / W2 decode matvecs   -> gpurun_out/r05_trace/
+#   prof65      the 65B decode under rocprofv3 --kernel-trace         -> gpurun_out/r05_prof65/
 #   ab13        13B Q4_1 decode with and without half-group work units -> gpurun_out/r05_ab13/
 set -o pipefail
 mkdir -p gpurun_out
@@ -18,6 +24,41 @@ for step in "$@"; do
   suite)
     timeout -k 10 900 $T tests/ > gpurun_out/gputests.log 2>&1
     rc=$?; grep -E "passed|failed" gpurun_out/gputests.log | tail -2; [ $rc -eq 0 ] || exit $rc ;;
+  bench)
+    timeout -k 10 900 python3 -u bench.py > gpurun_out/r05_bench.json 2> gpurun_out/r05_bench.err \
+      || { tail -20 gpurun_out/r05_bench.err; exit 21; }
+    tail -c 600 gpurun_out/r05_bench.json ;;
+  kt)
+    O=gpurun_out/r05_kt; mkdir -p $O
+    timeout -k 10 300 python3 tools/decode_speed.py 7b 8 > $O/gen.log 2>&1 || exit 31
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/kt7 -o run --output-format csv -- \
+      python3 bench.py --steps 96 --warmup 8 --no-13b --no-65b --no-cpu-baseline --prompt-evals 1 > $O/kt7.log 2>&1 || exit 32
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt13 -o run --output-format csv -- \
+      python3 tools/decode_speed.py 13b 64 > $O/kt13.log 2>&1 || exit 33
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/ktp -o run --output-format csv -- \
+      python3 tools/prompt_once.py > $O/ktp.log 2>&1 || exit 34
+    find $O -name '*kernel_stats.csv' ;;
+  pmc)
+    timeout -k 10 1000 bash tools/gpu_pmc_decode.sh gpurun_out/r05_traffic.json || exit 41 ;;
+  sq)
+    # one pass of 8 SQ counters over a short 7B decode: issue cycles of the five decode kernels
+    O=gpurun_out/r05_sq; mkdir -p $O
+    timeout -k 10 300 python3 tools/decode_speed.py 7b 8 > $O/gen.log 2>&1 || exit 51
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU \
+      SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS -d $O/sqA -o run --output-format csv -- \
+      python3 tools/decode_speed.py 7b 8 > $O/sqA.log 2>&1 || exit 52
+    timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_WAIT_INST_LDS \
+      -d $O/sqB -o run --output-format csv -- python3 tools/decode_speed.py 7b 8 > $O/sqB.log 2>&1 || exit 53
+    python3 tools/pmc_reduce.py $O/sq_decode_7b.json $(find $O/sqA $O/sqB -name '*counter_collection.csv') || exit 54
+    echo sq-ok ;;
+  split)
+    # the N > 1 65B leg rehearsed on one GPU: two ranks, one 40-layer stage each, shm stage link
+    timeout -k 10 600 python3 tools/decode_speed.py 65b 2 > gpurun_out/r05_split_gen.log 2>&1 || exit 61
+    timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29517 bench.py --gpus 2 --split-transport shm --no-13b --no-cpu-baseline \
+      > gpurun_out/r05_bench_split_shm_s2.json 2> gpurun_out/r05_split.err \
+      || { tail -30 gpurun_out/r05_split.err; exit 62; }
+    tail -c 800 gpurun_out/r05_bench_split_shm_s2.json ;;
   l2)
     O=gpurun_out/r05_l2; mkdir -p $O
     timeout -k 10 60 ./tools/probe/l2_probe xcc > $O/xcc.log 2>&1 || exit 11
@@ -30,77 +71,28 @@ for step in "$@"; do
       done
     done
     cat $O/xcc.log; grep -h mode $O/*.log ;;
+  trace)
+    # per-wave phase stamps (tools/probe/mv_probe_T, LVK_TRACE_RAW: events per wave index), kinds 2 wo, 4 w2
+    O=gpurun_out/r05_trace; mkdir -p $O
+    for k in 2 4; do
+      LVK_TRACE_RAW=1 LVK_TRACE_KIND=$k timeout -k 10 120 ./tools/probe/mv_probe_T 256 > $O/raw_$k.log 2>&1 || exit 71
+    done
+    cat $O/raw_*.log | grep -v "^exp check" ;;
+  prof65)
+    O=gpurun_out/r05_prof65; mkdir -p $O
+    timeout -k 10 600 python3 tools/decode_speed.py 65b 4 > $O/gen.log 2>&1 || exit 81
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
+      python3 tools/decode_speed.py 65b 16 > $O/kt65.log 2>&1 || exit 82
+    find $O -name '*kernel_stats.csv' ;;
   ab13)
     # 13B Q4_1 decode: half-group work units (LVK_MV41_HALF) A/B, twice each
     O=gpurun_out/r05_ab13; mkdir -p $O
     for r in 1 2; do
       for h in 0 1; do
         LVK_MV41_HALF=$h timeout -k 10 300 python3 tools/decode_speed.py 13b 64 2>/dev/null \
-          | sed "s/^{/{\"half\": $h, /" | tee -a $O/ab.jsonl || exit 41
+          | sed "s/^{/{\"half\": $h, /" | tee -a $O/ab.jsonl || exit 91
       done
     done ;;
-  diag65)
-    O=gpurun_out/r05_diag65; mkdir -p $O
-    timeout -k 10 600 python3 tools/decode_speed.py 65b 4 > $O/gen.log 2>&1 || exit 21
-    LVK_SEGV_TRACE=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
-      python3 tools/decode_speed.py 65b 16 > $O/kt65.log 2>&1
-    rc=$?; tail -5 $O/kt65.log; exit $rc ;;
-  prof65)
-    O=gpurun_out/r05_prof65; mkdir -p $O
-    timeout -k 10 600 python3 tools/decode_speed.py 65b 4 > $O/gen.log 2>&1 || exit 31
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
-      python3 tools/decode_speed.py 65b 16 > $O/kt65.log 2>&1 || exit 32
-    find $O -name '*kernel_stats.csv' ;;
-  pc)
-    # the producer / consumer decode matvec (Wo, W2): parity of the 7B-shaped / full 7B decode, then
-    # A/B speed and per-wave phase stamps
-    O=gpurun_out/r05_pc; mkdir -p $O
-    timeout -k 10 900 $T tests/test_gpu_model.py tests/test_gpu_decode_chain.py tests/test_gpu_7b_full.py \
-      > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 51; }
-    tail -2 $O/tests.log
-    for r in 1 2; do
-      for k in 0 1 2; do
-        LVK_MV_PC=$k timeout -k 10 300 python3 tools/decode_speed.py 7b 96 2>/dev/null \
-          | sed "s/^{/{\"pc\": $k, /" | tee -a $O/ab.jsonl || exit 52
-      done
-    done
-    for k in 2 4; do
-      for v in 1 2; do
-        LVK_MV_PC=$v LVK_TRACE_RAW=1 LVK_TRACE_KIND=$k timeout -k 10 120 ./tools/probe/mv_probe_T 256 > $O/raw_${k}_pc$v.log 2>&1 || exit 53
-      done
-    done
-    cat $O/raw_*.log | grep -v "^exp check" ;;
-  ks)
-    # the K-split decode matvec (Wo, W2): parity of the 7B-shaped / full 7B decode, then A/B speed
-    O=gpurun_out/r05_ks; mkdir -p $O
-    timeout -k 10 900 $T tests/test_gpu_model.py tests/test_gpu_decode_chain.py tests/test_gpu_7b_full.py \
-      > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 51; }
-    tail -2 $O/tests.log
-    for r in 1 2; do
-      for k in 0 1; do
-        LVK_MV_KS=$k timeout -k 10 300 python3 tools/decode_speed.py 7b 96 2>/dev/null \
-          | sed "s/^{/{\"ks\": $k, /" | tee -a $O/ab.jsonl || exit 52
-      done
-    done ;;
-  trace)
-    # per-wave phase stamps of the decode matvecs (tools/probe/mv_probe_T, LVK_TRACE_RAW: events per
-    # wave index), kinds 2 wo, 4 w2, with and without the K-split kernel
-    O=gpurun_out/r05_trace; mkdir -p $O
-    for k in 2 4; do
-      for ks in 0 1; do
-        LVK_MV_KS=$ks LVK_TRACE_RAW=1 LVK_TRACE_KIND=$k timeout -k 10 120 ./tools/probe/mv_probe_T 256 \
-          > $O/raw_${k}_ks$ks.log 2>&1 || exit 61
-      done
-    done
-    cat $O/raw_*.log | grep -v "^exp check" ;;
-  diag04)
-    # the round-4 library (lib/r04diag, built from commit 7eefa8d + the maps dump) under the
-    # kernel trace that crashed in round 4
-    O=gpurun_out/r05_diag04; mkdir -p $O
-    timeout -k 10 600 python3 tools/decode_speed.py 65b 4 > $O/gen.log 2>&1 || exit 71
-    LVK_SEGV_TRACE=1 LVK_LIB=$R/llama.vk_amd/lib/r04diag/libllama_vk_amd.so timeout -k 10 600 rocprofv3 --kernel-trace \
-      --stats -d $O/kt -o run --output-format csv -- python3 tools/r04diag/decode_speed.py 65b 16 > $O/kt65.log 2>&1
-    rc=$?; grep -v "^[EW]2026" $O/kt65.log | head -20; exit $rc ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done
