@@ -378,8 +378,18 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
         sv.x = Sv.x * dx.x; sv.y = Sv.y * dx.y; sv.z = Sv.z * dx.z; sv.w = Sv.w * dx.w;
         *(float4 *) (sw + buf * SPL + r * SRS + j * 4) = sv;
     };
+#ifndef LVK_PROBE_EXP
+#define LVK_PROBE_EXP 0
+#endif
+    // dev probe builds only (tools/probe mv_probe_xN): cost of the chain's parts.  1: four
+    // independent accumulators per lane instead of one serial chain; 2: no int -> float
+    // conversion (bit cast); 4: the scale products taken from registers, not the LDS table.
+    // None of these is bit-exact; the product build has LVK_PROBE_EXP = 0.
+    constexpr bool X_IND = (LVK_PROBE_EXP & 1) != 0, X_NOCVT = (LVK_PROBE_EXP & 2) != 0;
+    constexpr bool X_NOSA = (LVK_PROBE_EXP & 4) != 0;
     auto body = [&](auto has_next, int grp, int gnext) __attribute__((always_inline)) {
-        float acc = 0.0f;
+        float acc = 0.0f, acc1 = 0.0f, acc2 = 0.0f, acc3 = 0.0f;
+        auto cv = [](int p) __attribute__((always_inline)) { return X_NOCVT ? __int_as_float(p) : (float) p; };
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             const int slot = c % D;
@@ -399,7 +409,7 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
             float sa[8][4];
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
-                const float4 v = *(const float4 *) (sl + r * SRS + jj * 4);
+                const float4 v = X_NOSA ? S[slot] : *(const float4 *) (sl + r * SRS + jj * 4);
                 sa[jj][0] = v.x; sa[jj][1] = v.y; sa[jj][2] = v.z; sa[jj][3] = v.w;
             }
 #pragma unroll
@@ -414,10 +424,13 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
                         const int p1 = dot8(wd[2 * pp], a.y);
                         const int p2 = dot8(wd[2 * pp + 1], a.z);
                         const int p3 = dot8(wd[2 * pp + 1], a.w);
-                        acc = __builtin_fmaf(sa[(bi + 0) & 7][(bi + 0) >> 3], (float) p0, acc);
-                        acc = __builtin_fmaf(sa[(bi + 1) & 7][(bi + 1) >> 3], (float) p1, acc);
-                        acc = __builtin_fmaf(sa[(bi + 2) & 7][(bi + 2) >> 3], (float) p2, acc);
-                        acc = __builtin_fmaf(sa[(bi + 3) & 7][(bi + 3) >> 3], (float) p3, acc);
+                        acc = __builtin_fmaf(sa[(bi + 0) & 7][(bi + 0) >> 3], cv(p0), acc);
+                        float & a1 = X_IND ? acc1 : acc;
+                        a1 = __builtin_fmaf(sa[(bi + 1) & 7][(bi + 1) >> 3], cv(p1), a1);
+                        float & a2 = X_IND ? acc2 : acc;
+                        a2 = __builtin_fmaf(sa[(bi + 2) & 7][(bi + 2) >> 3], cv(p2), a2);
+                        float & a3 = X_IND ? acc3 : acc;
+                        a3 = __builtin_fmaf(sa[(bi + 3) & 7][(bi + 3) >> 3], cv(p3), a3);
                     }
                 }
             }
@@ -433,9 +446,11 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
             // keep chunks in program order: the chain value is pinned here, so
             // chunk c's arithmetic cannot sink below chunk c+1's reads
             asm volatile("" : "+v"(acc));
+            if constexpr (X_IND) asm volatile("" : "+v"(acc1), "+v"(acc2), "+v"(acc3));
             LVK_T(tq); ++tq;
             __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr (X_IND) acc = (acc + acc1) + (acc2 + acc3);
         return octet_reduce(acc);
     };
 

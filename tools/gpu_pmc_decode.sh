@@ -10,7 +10,7 @@ OUT=${1:-gpurun_out/pmc_decode/traffic.json}
 for m in 7b 13b; do
   timeout -k 10 300 python3 tools/decode_speed.py $m 8 > $O/gen_$m.log 2>&1 || exit 1
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 120 rocprofv3 --pmc $c -d $O/${m}_$c -o run --output-format csv -- python3 tools/decode_speed.py $m 8 > $O/${m}_$c.log 2>&1 || exit 2
+    env DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 timeout -s KILL 120 rocprofv3 --pmc $c -d $O/${m}_$c -o run --output-format csv -- python3 tools/decode_speed.py $m 8 > $O/${m}_$c.log 2>&1 || exit 2
     echo "pmc $m $c done"
   done
 done

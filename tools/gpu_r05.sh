@@ -17,6 +17,10 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 T="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
+# profiled runs: HIP's graph packet capture off.  rocprofv3's dispatch interception reads a
+# captured graph's packet batch past the end of the AQL ring when the batch wraps it (SIGSEGV
+# at the ring's end: profiles/r05/rocprof_graph_fault/README.md); unprofiled runs keep it on
+NOCAP=DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
 
 for step in "$@"; do
   echo "== step $step"
@@ -31,11 +35,11 @@ for step in "$@"; do
   kt)
     O=gpurun_out/r05_kt; mkdir -p $O
     timeout -k 10 300 python3 tools/decode_speed.py 7b 8 > $O/gen.log 2>&1 || exit 31
-    timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/kt7 -o run --output-format csv -- \
+    env $NOCAP timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/kt7 -o run --output-format csv -- \
       python3 bench.py --steps 96 --warmup 8 --no-13b --no-65b --no-cpu-baseline --prompt-evals 1 > $O/kt7.log 2>&1 || exit 32
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt13 -o run --output-format csv -- \
+    env $NOCAP timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt13 -o run --output-format csv -- \
       python3 tools/decode_speed.py 13b 64 > $O/kt13.log 2>&1 || exit 33
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/ktp -o run --output-format csv -- \
+    env $NOCAP timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/ktp -o run --output-format csv -- \
       python3 tools/prompt_once.py > $O/ktp.log 2>&1 || exit 34
     find $O -name '*kernel_stats.csv' ;;
   pmc)
@@ -44,10 +48,10 @@ for step in "$@"; do
     # one pass of 8 SQ counters over a short 7B decode: issue cycles of the five decode kernels
     O=gpurun_out/r05_sq; mkdir -p $O
     timeout -k 10 300 python3 tools/decode_speed.py 7b 8 > $O/gen.log 2>&1 || exit 51
-    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU \
+    env $NOCAP timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU \
       SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS -d $O/sqA -o run --output-format csv -- \
       python3 tools/decode_speed.py 7b 8 > $O/sqA.log 2>&1 || exit 52
-    timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_WAIT_INST_LDS \
+    env $NOCAP timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_WAIT_INST_LDS \
       -d $O/sqB -o run --output-format csv -- python3 tools/decode_speed.py 7b 8 > $O/sqB.log 2>&1 || exit 53
     python3 tools/pmc_reduce.py $O/sq_decode_7b.json $(find $O/sqA $O/sqB -name '*counter_collection.csv') || exit 54
     echo sq-ok ;;
@@ -59,6 +63,22 @@ for step in "$@"; do
       > gpurun_out/r05_bench_split_shm_s2.json 2> gpurun_out/r05_split.err \
       || { tail -30 gpurun_out/r05_split.err; exit 62; }
     tail -c 800 gpurun_out/r05_bench_split_shm_s2.json ;;
+  diag7)
+    # the 7B bench under the kernel trace with the fault dump (LVK_SEGV_TRACE: frames + maps)
+    O=gpurun_out/r05_diag7; mkdir -p $O
+    timeout -k 10 300 python3 tools/decode_speed.py 7b 4 > $O/gen.log 2>&1 || exit 101
+    # DIAG_ENV: extra environment of the profiled run (e.g. HSA_ENABLE_SDMA=0)
+    env LVK_SEGV_TRACE=1 $DIAG_ENV timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
+      python3 bench.py --steps 96 --warmup 8 --no-13b --no-65b --no-cpu-baseline --prompt-evals 1 > $O/kt7.log 2>&1
+    rc=$?; grep -v "^[EW]2026" $O/kt7.log | head -30; exit $rc ;;
+  x)
+    # chain-part costs (tools/probe mv_probe_xN, LVK_PROBE_EXP; not bit-exact) beside the product kernels
+    O=gpurun_out/r05_x; mkdir -p $O
+    for e in 0 1 2 4 7 0; do
+      b=./tools/probe/mv_probe_x$e; [ $e = 0 ] && b=./tools/probe/mv_probe
+      timeout -k 10 120 $b 256 > $O/x$e.log 2>&1 || exit 111
+      echo "exp $e: $(grep -E '^  (wo|w2|qkv|w13) ' $O/x$e.log | tr -s ' ' | tr '\n' ';')"
+    done ;;
   l2)
     O=gpurun_out/r05_l2; mkdir -p $O
     timeout -k 10 60 ./tools/probe/l2_probe xcc > $O/xcc.log 2>&1 || exit 11
@@ -66,7 +86,7 @@ for step in "$@"; do
       for mode in "cold 0" "hot 0" "hot 1" "pf 0" "pf 1"; do
         set -- $mode
         d=$O/${kind}_$1_$2
-        timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
+        env $NOCAP timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
           ./tools/probe/l2_probe $1 $kind $2 > $d.log 2>&1 || exit 12
       done
     done
@@ -81,9 +101,22 @@ for step in "$@"; do
   prof65)
     O=gpurun_out/r05_prof65; mkdir -p $O
     timeout -k 10 600 python3 tools/decode_speed.py 65b 4 > $O/gen.log 2>&1 || exit 81
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
+    env $NOCAP timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
       python3 tools/decode_speed.py 65b 16 > $O/kt65.log 2>&1 || exit 82
     find $O -name '*kernel_stats.csv' ;;
+  ab41)
+    # 13B Q4_1 decode: even-chain weight sums in the kernel (LVK_MV41_WSI=1) vs the weight-sum
+    # image; the Q4_1 parity tests with the in-kernel sums first
+    O=gpurun_out/r05_ab41; mkdir -p $O
+    LVK_MV41_WSI=1 timeout -k 10 600 $T tests/test_gpu_13b_full.py tests/test_gpu_model.py -k "q4_1 or 13b" \
+      > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 121; }
+    tail -2 $O/tests.log
+    for r in 1 2; do
+      for w in 0 1; do
+        LVK_MV41_WSI=$w timeout -k 10 300 python3 tools/decode_speed.py 13b 64 2>/dev/null \
+          | sed "s/^{/{\"wsi\": $w, /" | tee -a $O/ab.jsonl || exit 122
+      done
+    done ;;
   ab13)
     # 13B Q4_1 decode: half-group work units (LVK_MV41_HALF) A/B, twice each
     O=gpurun_out/r05_ab13; mkdir -p $O
