@@ -60,11 +60,7 @@ constexpr int SRS = 40, SPL = 8 * SRS, SWF = 4 * SPL;
 // halves of different groups' 1 KiB slices).  With M = 5120 (13B Wo, W2) every CU then streams
 // exactly 20 rows instead of 16 or 24 (640 groups on 256 CUs).  Not for the W1|W3 epilogue,
 // which pairs the w1 half of a group with its w3 half inside the wave.
-// WSI: the even chains' weight sums (ggml.c:2236-2240) are formed from the nibble words in the
-// kernel (wsum_word: nibble-pair bytes, two DPP quad adds, a half-row mirror) instead of read
-// from the weight-sum image -- 24 instead of 28 streamed bytes per 32 weights, exact integers
-// either way.
-template <int NW, int D, int PRO, int EPI, int KT, int SPLIT = 0, int HALF = 0, int WSI = 0>
+template <int NW, int D, int PRO, int EPI, int KT, int SPLIT = 0, int HALF = 0>
 __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     static_assert(!(HALF && EPI == EPI_SWIGLU_F32), "W1|W3 pairs the halves of one group");
     constexpr int nb = KT / 32;                 // blocks per row
@@ -164,7 +160,7 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
         const char * sc_ = (const char *) P.scl + (BS) + (cc) * 2048;                                   \
         SD[slot] = *(const float4 *) sc_;                                                               \
         SM[slot] = *(const float4 *) (sc_ + 1024);                                                      \
-        if constexpr (!WSI) WS[slot] = ld_nt((const uint4 *) ((const char *) P.wsum + (BW) + (cc) * 1024)); \
+        WS[slot] = ld_nt((const uint4 *) ((const char *) P.wsum + (BW) + (cc) * 1024));                 \
         __builtin_amdgcn_sched_barrier(0);                                                              \
     } while (0)
 #pragma unroll
@@ -239,8 +235,6 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
 
     // row groups: chunk loop with cross-group prefetch
     const bool even = (j & 1) == 0;
-    const bool wsi_other = j == 2 || j == 4;            // wsum_word: chain 2k's sum lives in the other quad
-    const uint32_t wsi_sh = j >= 4 ? 8u : 0u;
     const uint32_t * ys32 = (const uint32_t *) ys;
     float * sw = sbuf + wave * SWF;
     auto body = [&](auto has_next, float & off) __attribute__((always_inline)) {
@@ -276,13 +270,11 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
                 // take the precomputed weight sums (blocks 0-15 of the chunk in their own word,
                 // 16-31 in the odd neighbour's: DPP quad_perm [1,1,3,3]), odd chains the
                 // activation sums from LDS; one byte per block, exact as floats
-                uint32_t wown[4] = {0u, 0u, 0u, 0u}, wnb[4] = {0u, 0u, 0u, 0u};
-                if constexpr (!WSI) {
-                    wown[0] = WS[slot].x; wown[1] = WS[slot].y; wown[2] = WS[slot].z; wown[3] = WS[slot].w;
+                const uint32_t wown[4] = {WS[slot].x, WS[slot].y, WS[slot].z, WS[slot].w};
+                uint32_t wnb[4];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        wnb[q] = (uint32_t) __builtin_amdgcn_mov_dpp((int) wown[q], 0xF5, 0xF, 0xF, false);
-                }
+                for (int q = 0; q < 4; ++q)
+                    wnb[q] = (uint32_t) __builtin_amdgcn_mov_dpp((int) wown[q], 0xF5, 0xF, 0xF, false);
 #pragma unroll
                 for (int sb = 0; sb < 4; ++sb) {
                     if (c * 4 + sb < nsub) {
@@ -296,16 +288,7 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
                             const float4 x4 = *(const float4 *) (xrow + bi);
                             const float4 m4 = *(const float4 *) (mrow + bi);
                             const uint32_t ydw = ys32[(size_t) uu * 4 + (j >> 1)];
-                            uint32_t wdw;
-                            if constexpr (WSI) {
-                                // bytes 0 / 2: the sums of blocks bi, bi+1 (word 2pp) and bi+2, bi+3
-                                // (word 2pp+1), gathered to bytes 0..3 in block order
-                                const uint32_t x = wsum_word(wd[2 * pp], wsi_other, wsi_sh);
-                                const uint32_t y = wsum_word(wd[2 * pp + 1], wsi_other, wsi_sh);
-                                wdw = __builtin_amdgcn_perm(y, x, 0x06040200u);
-                            } else {
-                                wdw = sb < 2 ? wown[(sb & 1) * 2 + pp] : wnb[(sb & 1) * 2 + pp];
-                            }
+                            const uint32_t wdw = sb < 2 ? wown[(sb & 1) * 2 + pp] : wnb[(sb & 1) * 2 + pp];
                             const uint32_t sdw = even ? wdw : ydw;
                             const float S[4] = {(float) (sdw & 0xFFu), (float) ((sdw >> 8) & 0xFFu),
                                                 (float) ((sdw >> 16) & 0xFFu), (float) (sdw >> 24)};
@@ -375,12 +358,6 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
 #undef LVK_ISSUE41
 }
 
-// LVK_MV41_WSI=1: the even-chain weight sums formed in the kernel (A/B against the image)
-static bool wsi_env() {
-    static const bool v = [] { const char * e = getenv("LVK_MV41_WSI"); return e && atoi(e) != 0; }();
-    return v;
-}
-
 template <int NW, int D, int PRO, int EPI, int KT, int SPLIT = 0, int HALF = 0>
 hipError_t go(const Cu41Params & P, hipStream_t s) {
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
@@ -391,8 +368,7 @@ hipError_t go(const Cu41Params & P, hipStream_t s) {
     const int items = HALF ? ((2 * P.G + nwg - 1) / nwg + 1) / 2 : (P.G + nwg - 1) / nwg;
     if (!XG && items > NW) return hipErrorNotSupported;
     const size_t lds = (size_t) nb * 32 + 2 * NC * 128 + (size_t) nb * 16 + NW * SWF * 4 + NW * 8;
-    if (wsi_env()) LVK_LAUNCH((k_mv_cu41<NW, D, PRO, EPI, KT, SPLIT, HALF, 1>), dim3(nwg), dim3(NW * 64), lds, s, P);
-    else LVK_LAUNCH((k_mv_cu41<NW, D, PRO, EPI, KT, SPLIT, HALF, 0>), dim3(nwg), dim3(NW * 64), lds, s, P);
+    LVK_LAUNCH((k_mv_cu41<NW, D, PRO, EPI, KT, SPLIT, HALF>), dim3(nwg), dim3(NW * 64), lds, s, P);
     return hipGetLastError();
 }
 
