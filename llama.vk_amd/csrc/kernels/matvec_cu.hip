@@ -497,12 +497,15 @@ __global__ __launch_bounds__((NW + NP) * 64) void k_mv_cu(CuParams P) {
 
 // -- host -------------------------------------------------------------------
 
-// prologue order (k_mv_cu PF): PFD per launch shape (measured, tools/probe sweeps);
-// LVK_MV_PF=0..3 overrides it for A/B runs
+// prologue order (k_mv_cu PF): PFD per launch shape (measured, tools/probe sweeps); the sweep
+// probe build (LVK_PROBE_SWEEP) reads LVK_MV_PF=0..5 to override it for A/B runs, the product
+// library carries only the shipped order
+#ifdef LVK_PROBE_SWEEP
 static int mv_pf_env() {
     static const int v = [] { const char * e = getenv("LVK_MV_PF"); return e ? atoi(e) : -1; }();
     return v;
 }
+#endif
 
 template <int NW, int NP, int D, int PRO, int EPI, int KT, int PFD = 2>
 hipError_t go(const CuParams & P, hipStream_t s) {
@@ -512,6 +515,7 @@ hipError_t go(const CuParams & P, hipStream_t s) {
     // without cross-group prefetch every wave must own at most one group
     if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
     const size_t lds = (size_t) nb * 32 + NC * 128 + NW * 2 * SPL * 4 + NW * 8;
+#ifdef LVK_PROBE_SWEEP
     const int pf = mv_pf_env() >= 0 ? mv_pf_env() : PFD;
     switch (pf) {
         case 0: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 0>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
@@ -521,6 +525,9 @@ hipError_t go(const CuParams & P, hipStream_t s) {
         case 4: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 4>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
         default: LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 5>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P); break;
     }
+#else
+    LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, PFD>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
+#endif
     return hipGetLastError();
 }
 
@@ -609,7 +616,7 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
         if (epi == EPI_STORE && pro == PRO_ACTF) return go<8, 0, 2, PRO_ACTF, EPI_STORE, 4096>(P, s);
     } else if (K == 8192) {
         switch (epi) {
-            // prologue orders on the 65B shapes (tools/gpu_pf65.sh, profiles/r03_pf65.txt): 0 for
+            // prologue orders on the 65B shapes (round-3 sweep, profiles/r03_pf65.txt): 0 for
             // QKV / W1|W3 (22.4 / 38.6 vs 23.1 / 40.1 us at order 2), 5 for Wo (8.2 vs 8.4)
             case EPI_QKV: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_QKV, 8192, 0>(P, s); break;
             case EPI_SWIGLU_F32: if (pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 8192, 0>(P, s); break;
