@@ -664,7 +664,8 @@ def run(args, coord):
     coord.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        lg = m.eval([tok], pos_of(i))
+        # llama_eval + argmax over llama_get_logits' row, as examples/main reads it (no copy)
+        lg = m.eval([tok], pos_of(i), copy=False)
         tok = int(np.argmax(lg[-1]))
     t1 = time.perf_counter()
     coord.barrier()

@@ -607,20 +607,8 @@ void Context::begin_eval(const int * tokens, int n, int n_past, const EvalPart &
     }
 }
 
-// LVK_SYNC_SPIN=1: end_eval polls the stream instead of a blocking synchronize (A/B of the
-// host wake-up latency per token)
-static bool sync_spin() {
-    static const bool v = [] { const char * e = getenv("LVK_SYNC_SPIN"); return e && atoi(e) != 0; }();
-    return v;
-}
-
 void Context::end_eval(bool no_host_logits) {
     sp_next = 1;
-    if (sync_spin()) {
-        hipError_t q;
-        while ((q = hipStreamQuery(stream)) == hipErrorNotReady) {}
-        LVK_HIP(q);
-    }
     LVK_HIP(hipStreamSynchronize(stream));
     if (profiling) collect_profile();
     check_device_error();

@@ -182,11 +182,13 @@ class Llama:
         self.n_ctx = lib.llama_n_ctx(self.ctx)
         self._last_n = 1
 
-    def eval(self, tokens, n_past, n_threads=1):
+    def eval(self, tokens, n_past, n_threads=1, copy=True):
+        """llama_eval; returns the logits rows (copy=False: a read-only view of the context's
+        host buffer, valid until the next eval -- what a C caller of llama_get_logits holds)"""
         t = np.ascontiguousarray(tokens, np.int32)
         _check(lib.llama_eval(self.ctx, t, len(t), n_past, n_threads), "llama_eval")
         self._last_n = len(t)
-        return self.logits()
+        return self.logits(copy)
 
     def kv_cache_token_count(self):
         return lib.llama_get_kv_cache_token_count(self.ctx)
@@ -276,10 +278,14 @@ class Llama:
         n = lib.lvk_stage_layers(self.ctx, C.byref(b), C.byref(e))
         return b.value, e.value, n
 
-    def logits(self):
+    def logits(self, copy=True):
         rows = self._last_n if self.logits_all else 1
         ptr = lib.llama_get_logits(self.ctx)
-        return np.ctypeslib.as_array(ptr, shape=(rows * self.n_vocab,)).reshape(rows, self.n_vocab).copy()
+        v = np.ctypeslib.as_array(ptr, shape=(rows * self.n_vocab,)).reshape(rows, self.n_vocab)
+        if copy:
+            return v.copy()
+        v.flags.writeable = False
+        return v
 
     def embeddings(self):
         return np.ctypeslib.as_array(lib.llama_get_embeddings(self.ctx), shape=(self.n_embd,)).copy()

@@ -117,16 +117,6 @@ for step in "$@"; do
           | sed "s/^{/{\"wsi\": $w, /" | tee -a $O/ab.jsonl || exit 122
       done
     done ;;
-  spin)
-    # per-token host round trip: blocking stream synchronize vs polling (LVK_SYNC_SPIN), 7B bench legs
-    O=gpurun_out/r05_spin; mkdir -p $O
-    for r in 1 2; do
-      for v in 0 1; do
-        LVK_SYNC_SPIN=$v timeout -k 10 400 python3 bench.py --no-13b --no-65b --no-cpu-baseline --prompt-evals 1 \
-          > $O/b_${v}_${r}.json 2> $O/b_${v}_${r}.err || exit 131
-        python3 -c "import json,sys; d=json.loads(open('$O/b_${v}_${r}.json').read().splitlines()[-1]); g=d['decode_greedy_device']; print(json.dumps({'spin': $v, 'eval_loop': d['value'], 'greedy': g['value'], 'chained': g['chained']['value']}))" | tee -a $O/ab.jsonl
-      done
-    done ;;
   ab13)
     # 13B Q4_1 decode: half-group work units (LVK_MV41_HALF) A/B, twice each
     O=gpurun_out/r05_ab13; mkdir -p $O
