@@ -58,6 +58,7 @@ constexpr int TM = 128;     // rows per workgroup
 constexpr int TN = 16;      // tokens per workgroup (one token tile)
 constexpr int NT = 256;     // threads (4 waves)
 // LVK_MM_EXP (dev probe builds only, tools/probe), bit flags: 1 no fp32 chains, 2 no MFMA, 4 no B loads,
+// 64 no B stage global loads (LDS B path), 128 no scale outer-product MFMA, 256 no loop barriers,
 // 8 no A loads, 16 / 32 L2-hot A / B (below)
 #ifndef LVK_MM_EXP
 #define LVK_MM_EXP 0
@@ -337,7 +338,11 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
     uint4 bs0, bs1, bs2, bs3;                  // (named: an array of them stays in scratch)
     auto stage_load = [&](int u) {
         const uint4 * g = bsp + (size_t) u * 1024;
-        bs0 = g[0]; bs1 = g[NT]; bs2 = g[2 * NT]; bs3 = g[3 * NT];
+        if (LVK_MM_EXP & 64) {
+            bs0 = make_uint4(u, 1, 2, 3); bs1 = make_uint4(u, 5, 6, 7); bs2 = make_uint4(u, 9, 1, 2); bs3 = make_uint4(u, 3, 4, 5);
+        } else {
+            bs0 = g[0]; bs1 = g[NT]; bs2 = g[2 * NT]; bs3 = g[3 * NT];
+        }
     };
     auto stage_store = [&](int u) {
         uint4 * bl = (uint4 *) (smem + ((u & 1) ? OFF_B1 : OFF_B0)) + tid;
@@ -421,7 +426,12 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
                 const int jc = (u & 3) * 8 + jb + h;        // block of the chunk this lane half feeds
                 const float dwa = wl[jc * DWS + 32 * w + rho];
                 const float dab = dl[jc * DAS + (lane & 15)];
-                SC = __builtin_amdgcn_mfma_f32_32x32x1f32(dwa, dab, (f32x32_t){}, 0, 0, 0);
+                if (LVK_MM_EXP & 128) {
+#pragma unroll
+                    for (int i = 0; i < 32; ++i) SC[i] = dwa + dab;
+                } else {
+                    SC = __builtin_amdgcn_mfma_f32_32x32x1f32(dwa, dab, (f32x32_t){}, 0, 0, 0);
+                }
             }
             float sc[16];
 #pragma unroll
@@ -456,7 +466,7 @@ __global__ __launch_bounds__(NT, 2) void k_mm_q40_mfma(MmParams P) {
         if (!A16 && u + 1 < U) make_x(Anext);
         if (BL && u + 1 < U) stage_store(u + 1);
         if (scales_next) store_scales(ch + 1);
-        if (scales_next || (BL && u + 1 < U))
+        if ((scales_next || (BL && u + 1 < U)) && !(LVK_MM_EXP & 256))
             __syncthreads();            // chunk ch+1's scales / sub-chunk u+1's B visible; the buffers of
                                         // chunk ch-1 / sub-chunk u-1 free again
     }

@@ -121,7 +121,7 @@ for step in "$@"; do
     # prompt matmul knockouts on the 7B shapes, N = 512, f16 A image (tools/probe/mm_probe_expN,
     # LVK_MM_EXP bits: 1 no fp32 chains, 2 no MFMA, 8 no A loads; timing only)
     O=gpurun_out/r05_mmx; mkdir -p $O
-    for e in 0 1 2 3 8 9 10 11; do
+    for e in ${MMX:-0 1 2 3 8 9 10 11}; do
       b=./tools/probe/mm_probe_exp$e; [ $e = 0 ] && b=./tools/probe/mm_probe
       MM_A16=1 timeout -k 10 120 $b 512 20 > $O/x$e.log 2>&1 || exit 141
       echo "exp $e: $(tr -s ' ' < $O/x$e.log | tr '\n' ';')"
