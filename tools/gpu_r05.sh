@@ -126,6 +126,15 @@ for step in "$@"; do
       MM_A16=1 timeout -k 10 120 $b 512 20 > $O/x$e.log 2>&1 || exit 141
       echo "exp $e: $(tr -s ' ' < $O/x$e.log | tr '\n' ';')"
     done ;;
+  mmab)
+    # prompt matmul A/B: probe builds named in MMB (tools/probe/<name>), twice each; hashes must match
+    O=gpurun_out/r05_mmab; mkdir -p $O
+    for r in 1 2; do
+      for b in ${MMB:-mm_probe}; do
+        MM_A16=1 timeout -k 10 120 ./tools/probe/$b 512 20 > $O/${b}_$r.log 2>&1 || exit 161
+        echo "$b: $(grep -o 'hash [0-9a-f]*\|[0-9.]* us [0-9]\|32 layers [0-9.]* ms' $O/${b}_$r.log | tr '\n' ' ')"
+      done
+    done ;;
   ab13)
     # 13B Q4_1 decode: half-group work units (LVK_MV41_HALF) A/B, twice each
     O=gpurun_out/r05_ab13; mkdir -p $O
