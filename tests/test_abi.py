@@ -125,3 +125,33 @@ def test_quantize_tool_matches_reference(lvk, ref, tmp_path, itype):
     ref.lib.llama_model_quantize.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
     assert ref.lib.llama_model_quantize(src.encode(), b.encode(), itype) == 0
     assert open(a, "rb").read() == open(b, "rb").read()
+
+
+def test_logits_digest_c_abi_matches_numpy_twin(lvk):
+    """lvk_logits_digest (the host twin of the chained decode's device digest, include/lvk_ops.h)
+    equals lvk.logits_digest bit for bit, on rows with the special values a logits row can hold
+    (+-0, +-inf, NaN, denormals), and is order- and bit-sensitive"""
+    rng = np.random.RandomState(11)
+    rows = [rng.standard_normal(32000).astype(np.float32) * 8,
+            np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 3.4e38], np.float32),
+            np.zeros(5, np.float32), np.ones(1, np.float32)]
+    for row in rows:
+        got = lvk.lib.lvk_logits_digest(np.ascontiguousarray(row), len(row))
+        assert got == lvk.logits_digest(row)
+    r = rows[0].copy()
+    base = lvk.logits_digest(r)
+    r[[5, 9]] = r[[9, 5]]
+    assert lvk.logits_digest(r) != base                      # a swapped pair changes it
+    r = rows[0].copy()
+    r.view(np.uint32)[123] ^= 1                               # one ulp anywhere changes it
+    assert lvk.lib.lvk_logits_digest(r, len(r)) != base
+    assert lvk.lib.lvk_logits_digest(rows[0], 0) == 0         # empty row
+
+
+def test_forced_tokens_are_seeded_non_repeating_ids():
+    """the teacher-forced streams of the chained checks (tests/oracle_lib.forced_tokens)"""
+    import oracle_lib
+    a = oracle_lib.forced_tokens(496)
+    assert len(set(a.tolist())) == 496 and a.min() >= 3 and a.max() < 32000
+    assert np.array_equal(a, oracle_lib.forced_tokens(496))
+    assert not np.array_equal(a, oracle_lib.forced_tokens(496, seed=6))
