@@ -71,9 +71,10 @@ def test_13b_q4_1_full_prompt512_vs_reference(model13b, ref):
     rm.close()
 
 
-def test_13b_q4_1_full_context_decode_to_271_vs_reference(model13b, ref):
-    """BASELINE configs[3] at growing context: 256 teacher-forced decode steps (n_past 16..271,
-    through the score-exchange attention path and n_kv 256/257), every step's logits bit-identical
-    to the reference build, the chained per-step digests equal to the reference's"""
+def test_13b_q4_1_full_context_decode_to_511_vs_reference(model13b, ref):
+    """BASELINE configs[3] over the whole window: 496 teacher-forced decode steps (n_past 16..511,
+    the no-exchange attention path to n_kv 128 and the score exchange beyond, up to n_kv 512),
+    every step's logits bit-identical to the reference build, the chained per-step digests equal
+    to the reference's"""
     from test_gpu_7b_full import _full_context
-    _full_context(model13b, ref, 271)
+    _full_context(model13b, ref, 511)
