@@ -135,6 +135,22 @@ for step in "$@"; do
         echo "$b: $(grep -o 'hash [0-9a-f]*\|[0-9.]* us [0-9]\|32 layers [0-9.]* ms' $O/${b}_$r.log | tr '\n' ' ')"
       done
     done ;;
+  envab)
+    # A/B of one environment switch (ABVAR, values ABVALS, default 0 1) on the 7B bench legs, twice;
+    # with ABTESTS set, those GPU tests run first with the last value
+    O=gpurun_out/r05_envab_$ABVAR; mkdir -p $O
+    vals=${ABVALS:-0 1}
+    if [ -n "$ABTESTS" ]; then
+      env $ABVAR=${vals##* } timeout -k 10 900 $T $ABTESTS > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 171; }
+      tail -2 $O/tests.log
+    fi
+    for r in 1 2; do
+      for v in $vals; do
+        env $ABVAR=$v timeout -k 10 400 python3 bench.py --no-13b --no-65b --no-cpu-baseline --prompt-evals 1 \
+          > $O/b_${v}_${r}.json 2> $O/b_${v}_${r}.err || exit 172
+        python3 -c "import json,sys; d=json.loads(open('$O/b_${v}_${r}.json').read().splitlines()[-1]); g=d['decode_greedy_device']; print(json.dumps({'$ABVAR': '$v', 'eval_loop': round(d['value'],1), 'greedy': round(g['value'],1), 'chained': round(g['chained']['value'],1), 'sampled_dev': round(g['sampled_decode_tok_s']['device_sampler'],1)}))" | tee -a $O/ab.jsonl
+      done
+    done ;;
   ab13)
     # 13B Q4_1 decode: half-group work units (LVK_MV41_HALF) A/B, twice each
     O=gpurun_out/r05_ab13; mkdir -p $O
