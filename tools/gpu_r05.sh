@@ -28,6 +28,10 @@ for step in "$@"; do
   suite)
     timeout -k 10 900 $T tests/ > gpurun_out/gputests.log 2>&1
     rc=$?; grep -E "passed|failed" gpurun_out/gputests.log | tail -2; [ $rc -eq 0 ] || exit $rc ;;
+  smoke)
+    timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke-ok')" > gpurun_out/r05_smoke.log 2>&1 \
+      || { tail -20 gpurun_out/r05_smoke.log; exit 25; }
+    tail -2 gpurun_out/r05_smoke.log ;;
   bench)
     timeout -k 10 900 python3 -u bench.py > gpurun_out/r05_bench.json 2> gpurun_out/r05_bench.err \
       || { tail -20 gpurun_out/r05_bench.err; exit 21; }
