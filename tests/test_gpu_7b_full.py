@@ -121,3 +121,31 @@ def test_7b_full_context_decode_to_511_vs_reference(model7b, ref):
     """BASELINE configs[1] over the whole n_ctx 512 window: 496 teacher-forced decode steps
     (n_past 16..511)"""
     _full_context(model7b, ref, 511)
+
+
+def test_7b_long_context_2048_vs_reference(model7b, ref):
+    """n_ctx 2048, the LLaMA context length: a 1536-token prompt in 512-token batches (the
+    MFMA prompt path and the prompt attention at n_past 0 / 512 / 1024), then 512 teacher-forced
+    decode steps at n_past 1536..2047 (the decode attention at n_kv 1537..2048: 24-32 score chunks
+    per head exchanged between its 4 workgroups); every batch's last row and every step's logits
+    bit-identical to the reference build"""
+    import lvk
+    from oracle_lib import forced_tokens, prompt_tokens
+    m = lvk.Llama(model7b, n_ctx=2048)
+    rm = ref.model(model7b, 2048)
+    toks = prompt_tokens(1536)
+    for c in range(3):
+        part = toks[512 * c:512 * (c + 1)]
+        a = m.eval(part, 512 * c)
+        b = rm.eval(part, 512 * c, n_threads=_threads())
+        assert np.array_equal(bits(a[-1]), bits(b[-1])), "prompt batch %d logits differ" % c
+    seq = forced_tokens(512)
+    bad = []
+    for i, n_past in enumerate(range(1536, 2048)):
+        a = m.eval([int(seq[i])], n_past)
+        b = rm.eval([int(seq[i])], n_past, n_threads=_threads())
+        if not np.array_equal(bits(a[-1]), bits(b[-1])):
+            bad.append(n_past)
+    assert not bad, "decode logits differ at n_past %s" % bad[:20]
+    m.close()
+    rm.close()
