@@ -155,6 +155,21 @@ for step in "$@"; do
         python3 -c "import json,sys; d=json.loads(open('$O/b_${v}_${r}.json').read().splitlines()[-1]); g=d['decode_greedy_device']; print(json.dumps({'$ABVAR': '$v', 'eval_loop': round(d['value'],1), 'greedy': round(g['value'],1), 'chained': round(g['chained']['value'],1), 'sampled_dev': round(g['sampled_decode_tok_s']['device_sampler'],1)}))" | tee -a $O/ab.jsonl
       done
     done ;;
+  libab)
+    # library A/B: llama.vk_amd/lib/ab_base (the previous build) vs the tree's library, decode_speed on
+    # ABMODEL (default 13b), twice each; with ABTESTS set those GPU tests run first on the tree's library
+    O=gpurun_out/r05_libab; mkdir -p $O
+    if [ -n "$ABTESTS" ]; then
+      timeout -k 10 900 $T $ABTESTS > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 181; }
+      tail -2 $O/tests.log
+    fi
+    for r in 1 2; do
+      for l in base tree; do
+        if [ $l = base ]; then LIBV=$R/llama.vk_amd/lib/ab_base/libllama_vk_amd.so; else LIBV=; fi
+        env ${LIBV:+LVK_LIB=$LIBV} timeout -k 10 300 python3 tools/decode_speed.py ${ABMODEL:-13b} 64 2>/dev/null \
+          | sed "s/^{/{\"lib_ab\": \"$l\", /" | tee -a $O/ab.jsonl || exit 182
+      done
+    done ;;
   ab13)
     # 13B Q4_1 decode: half-group work units (LVK_MV41_HALF) A/B, twice each
     O=gpurun_out/r05_ab13; mkdir -p $O
