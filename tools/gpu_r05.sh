@@ -5,7 +5,7 @@
 #   kt          kernel-trace summaries: 7B bench legs, 13B Q4_1 decode, 7B 512-token prompt
 #                                                                     -> gpurun_out/r05_kt/
 #   pmc         FETCH_SIZE / WRITE_SIZE per decode kernel, 7B and 13B -> gpurun_out/r05_traffic.json
-#   sq          SQ issue / wait counters per decode kernel (7B)       -> gpurun_out/r05_sq/sq_decode_7b.json
+#   sq          SQ issue / wait counters per decode kernel (SQMODEL, 7b) -> gpurun_out/r05_sq_<m>/sq_decode_<m>.json
 #   split       65B layer split over 2 ranks on the one GPU through the shm stage link
 #                                                                     -> gpurun_out/r05_bench_split_shm_s2.json
 #   l2          L2 retention across launches (tools/probe/l2_probe)   -> gpurun_out/r05_l2/
@@ -50,14 +50,15 @@ for step in "$@"; do
     timeout -k 10 1000 bash tools/gpu_pmc_decode.sh gpurun_out/r05_traffic.json || exit 41 ;;
   sq)
     # one pass of 8 SQ counters over a short 7B decode: issue cycles of the five decode kernels
-    O=gpurun_out/r05_sq; mkdir -p $O
-    timeout -k 10 300 python3 tools/decode_speed.py 7b 8 > $O/gen.log 2>&1 || exit 51
+    M=${SQMODEL:-7b}
+    O=gpurun_out/r05_sq_$M; mkdir -p $O
+    timeout -k 10 300 python3 tools/decode_speed.py $M 8 > $O/gen.log 2>&1 || exit 51
     env $NOCAP timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU \
       SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS -d $O/sqA -o run --output-format csv -- \
-      python3 tools/decode_speed.py 7b 8 > $O/sqA.log 2>&1 || exit 52
+      python3 tools/decode_speed.py $M 8 > $O/sqA.log 2>&1 || exit 52
     env $NOCAP timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_WAIT_INST_LDS \
-      -d $O/sqB -o run --output-format csv -- python3 tools/decode_speed.py 7b 8 > $O/sqB.log 2>&1 || exit 53
-    python3 tools/pmc_reduce.py $O/sq_decode_7b.json $(find $O/sqA $O/sqB -name '*counter_collection.csv') || exit 54
+      -d $O/sqB -o run --output-format csv -- python3 tools/decode_speed.py $M 8 > $O/sqB.log 2>&1 || exit 53
+    python3 tools/pmc_reduce.py $O/sq_decode_$M.json $(find $O/sqA $O/sqB -name '*counter_collection.csv') || exit 54
     echo sq-ok ;;
   split)
     # the N > 1 65B leg rehearsed on one GPU: two ranks, one 40-layer stage each, shm stage link
