@@ -324,6 +324,7 @@ def cpu_baseline(path, budget_s=20.0, label="7B Q4_0", prompt=True, seg_steps=16
 SPLIT_TIMEOUT_S = 420
 SPLIT_FIRST_TOKEN = 1000       # the greedy token the split's first decode step embeds
 SPLIT_FORCED_STEPS = 16        # teacher-forced steps whose logits digests the split must reproduce
+SPLIT_LINK_LAPS = 64           # laps of the link probe (per_hop_us)
 
 
 def split_child(args):
@@ -363,6 +364,9 @@ def split_child(args):
         toks.append(tok)
         n_past = n_past + 1 if n_past + 1 < 512 else 16
     dec = time.perf_counter() - t0
+    # the link alone (lvk_stage_link_probe): one token's residual stream around the stage ring,
+    # SURVEY.md 8d's per-hop time; every stage takes part
+    hop_us = st.stage_link_probe(hp["n_embd"] * 4, SPLIT_LINK_LAPS)
     # a 512-token prompt through the pipeline, with and without micro-batches (every rank
     # times its own stage_step; the last stage's time is the pipeline's)
     p512 = np.array(prompt_tokens(512), np.int32)
@@ -386,7 +390,7 @@ def split_child(args):
         if s == S - 1:
             fdig.append(lvk.logits_digest(st.logits()[-1]))
     st.close()
-    print(json.dumps({"stage": s, "layers": list(lr), "load_s": load_s, "decode_s": dec,
+    print(json.dumps({"stage": s, "layers": list(lr), "load_s": load_s, "decode_s": dec, "hop_us": hop_us,
                       "prefill_s": pre[args.split_micro], "prefill_nomicro_s": pre[0],
                       "tokens": toks if first else None, "prompt_logits_digest": lhash,
                       "forced_digests": [str(d) for d in fdig] if s == S - 1 else None}), flush=True)
@@ -457,6 +461,7 @@ def layer_split(args, coord):
     if not ok:
         return {"error": err or "another rank's stage failed", "transport": args.split_transport}
     dec = coord.max(res["decode_s"])
+    hop_us = coord.max(res["hop_us"])
     pre = coord.max(res["prefill_s"])
     pre0 = coord.max(res["prefill_nomicro_s"])
     digest_split = coord.gather(res.get("prompt_logits_digest"))[-1]     # the last stage's
@@ -478,6 +483,11 @@ def layer_split(args, coord):
     coord.barrier()
     L = CFG_65B["n_layer"]
     r = args.steps_split / dec
+    hops = {"per_hop_us": hop_us, "message_bytes": CFG_65B["n_embd"] * 4, "laps": SPLIT_LINK_LAPS,
+            "hops_per_token": ws,
+            "method": "lvk_stage_link_probe: laps of one token's residual stream (n_embd f32) around the stage "
+                      "ring on the stage link's transport and stream, wall time per lap over the stages (max "
+                      "over ranks)"}
     transport = ("RCCL (ncclCommInitRank over the %d ranks)" % ws if args.split_transport == "rccl" else
                  "host shared-memory ring (lvk_stage_connect_shm; the one-GPU rehearsal of the RCCL link)")
     return {"value": r, "unit": "tok/s", "stages": ws, "steps": args.steps_split, "ms_per_token": 1e3 / r,
@@ -488,6 +498,7 @@ def layer_split(args, coord):
             "frac_hbm_roofline_1gpu": r * MODEL_BYTES_65B / 1e9 / HBM_PEAK_GBS,
             "prefill_512": {"tok_s": 512 / pre, "ms": pre * 1e3, "micro_batch": args.split_micro,
                             "tok_s_no_micro_batch": 512 / pre0},
+            "link": hops,
             "transport": transport, "devices": "rank r on device LOCAL_RANK %% %d" % lvk.device_count(),
             "greedy_check": check}
 

@@ -204,6 +204,13 @@ LVK_API int lvk_stage_connect(struct llama_context * ctx, const void * id, int n
 LVK_API int lvk_stage_connect_shm(struct llama_context * ctx, const char * name, int n_stages, int stage);
 LVK_API int lvk_stage_step(struct llama_context * ctx, const int * tokens, int n_tokens, int n_past, int greedy,
                            int micro);
+/* The stage link alone (per-hop time of the 65B split): `iters` laps of a `bytes`
+ * message (one token's residual stream is n_embd * 4) around the stage ring -- stage 0 sends
+ * to 1, ..., the last stage back to 0 -- on the same transport and stream as lvk_stage_step;
+ * every stage calls it.  *us_per_hop: the wall time of a lap over the number of stages.  0 on
+ * success, -1 on error (the link is aborted as in lvk_stage_step).  No reference counterpart:
+ * the reference has no inter-device hop (llama.cpp:927-1197 runs every layer in one process). */
+LVK_API int lvk_stage_link_probe(struct llama_context * ctx, int bytes, int iters, double * us_per_hop);
 
 /* ggml_graph_compute keeps the host ranges of its tensors mirrored in HBM across calls and
  * uploads only bytes a node reads before the call writes them, and of those only pages the

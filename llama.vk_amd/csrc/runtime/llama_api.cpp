@@ -477,6 +477,17 @@ int lvk_stage_step(struct llama_context * ctx, const llama_token * tokens, int n
     }
 }
 
+int lvk_stage_link_probe(struct llama_context * ctx, int bytes, int iters, double * us_per_hop) {
+    try {
+        if (bytes <= 0 || !us_per_hop) throw lvk::Error("llama.vk_amd: bad link probe arguments");
+        *us_per_hop = lvk::stage_link_probe(ctx->c, (size_t) bytes, iters);
+    } catch (const lvk::Error & e) {
+        fprintf(stderr, "%s: %s\n", __func__, e.msg.c_str());
+        return -1;
+    }
+    return 0;
+}
+
 void llama_free(struct llama_context * ctx) { delete ctx; }
 
 int llama_eval(struct llama_context * ctx, const llama_token * tokens, int n_tokens, int n_past, int n_threads) {

@@ -505,6 +505,37 @@ std::unique_ptr<StageTransport> make_shm_transport(const char * name, int n_stag
     return t;
 }
 
+double stage_link_probe(Context & c, size_t bytes, int iters) {
+    if (!c.link || !c.link->t) throw Error("llama.vk_amd: stage not connected (lvk_stage_connect)");
+    StageLink & L = *c.link;
+    StageTransport & T = *L.t;
+    const int s = L.stage, S = L.n_stages;
+    if (S < 2) throw Error("llama.vk_amd: the link probe needs two stages or more");
+    if (iters <= 0 || bytes == 0 || bytes > (size_t) c.n_ctx * c.model.hp.n_embd * sizeof(float))
+        throw Error("llama.vk_amd: bad link probe size");
+    DeviceGuard g(c.device);
+    auto lap = [&]() {
+        if (s == 0) {
+            T.send(c.x, bytes, 1, c.stream);
+            T.recv(c.x, bytes, S - 1, c.stream);
+        } else {
+            T.recv(c.x, bytes, s - 1, c.stream);
+            T.send(c.x, bytes, (s + 1) % S, c.stream);
+        }
+        T.wait(c.stream);
+    };
+    try {
+        for (int i = 0; i < 3; ++i) lap();
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < iters; ++i) lap();
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        return us / iters / S;
+    } catch (const Error &) {
+        T.abort();
+        throw;
+    }
+}
+
 int stage_step(Context & c, const int * tokens, int n, int n_past, bool greedy, int micro) {
     if (!c.link || !c.link->t) throw Error("llama.vk_amd: stage not connected (lvk_stage_connect)");
     StageLink & L = *c.link;

@@ -112,5 +112,8 @@ double stage_timeout_s();
 // lvk_stage_step: one eval of this rank's stage between its neighbours; returns the next
 // greedy token on the first and last stage when greedy, else 0
 int stage_step(Context & c, const int * tokens, int n, int n_past, bool greedy, int micro);
+// the link alone: `iters` laps of a `bytes` message around the stage ring (stage 0 sends to 1,
+// ..., the last stage back to 0), every stage taking part; returns microseconds per hop
+double stage_link_probe(Context & c, size_t bytes, int iters);
 
 }  // namespace lvk

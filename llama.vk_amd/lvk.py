@@ -125,6 +125,7 @@ _sig("lvk_rccl_unique_id", C.c_int, [C.c_void_p, C.c_size_t])
 _sig("lvk_stage_connect", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int])
 _sig("lvk_stage_connect_shm", C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.c_int])
 _sig("lvk_stage_step", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int])
+_sig("lvk_stage_link_probe", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)])
 _sig("lvk_init_split", C.c_void_p, [C.c_char_p, llama_context_params, C.c_int, i32p, C.c_char_p, C.c_int])
 _sig("lvk_split_info", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)])
 
@@ -261,6 +262,13 @@ class Llama:
         """join a one-stage-per-process pipeline over a host shared-memory ring
         (lvk_stage_connect_shm): returns once every stage has opened `name`"""
         _check(lib.lvk_stage_connect_shm(self.ctx, name.encode(), int(n_stages), int(stage)), "lvk_stage_connect_shm")
+
+    def stage_link_probe(self, nbytes, iters=64):
+        """microseconds per hop of the connected stage link (lvk_stage_link_probe; every stage
+        calls it)"""
+        us = C.c_double(0.0)
+        _check(lib.lvk_stage_link_probe(self.ctx, int(nbytes), int(iters), C.byref(us)), "lvk_stage_link_probe")
+        return us.value
 
     def stage_step(self, tokens, n_tokens, n_past, greedy=False, micro=64):
         """recv inpL -> this stage's layers -> send (lvk_stage_step); the greedy token on the

@@ -53,6 +53,10 @@ def main():
         toks.append(tok)
     res["fail_s"] = time.time() - t0
     res["tokens"] = np.array(toks, np.int32)
+    if mode == "run" and failed_at < 0:
+        # the link alone (lvk_stage_link_probe), then one more greedy step over the same link
+        res["hop_us"] = st.stage_link_probe(hp["n_embd"] * 4, 16)
+        res["post_probe_token"] = st.stage_step([tok] if first else None, 1, len(PROMPT) + 10, greedy=True)
     res["failed_at"] = failed_at
     st.close()
     np.savez(out, **res)

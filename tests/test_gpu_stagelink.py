@@ -69,6 +69,10 @@ def test_stage_processes_match_single_context(tiny_models, gpu_available, tmp_pa
     assert list(res[0]["tokens"]) == want_toks
     assert list(res[-1]["tokens"]) == want_toks
     assert all(r["failed_at"] == -1 for r in res)
+    # the link probe (lvk_stage_link_probe) ran on every stage and left the link usable: the
+    # next greedy step's token reached stage 0 from the last stage
+    assert all(0.0 < float(r["hop_us"]) < 1e6 for r in res)
+    assert int(res[0]["post_probe_token"]) == int(res[-1]["post_probe_token"])
 
 
 @pytest.mark.gpu
