@@ -12,6 +12,10 @@
 #   trace       per-wave phase stamps of the Wo / W2 decode matvecs   -> gpurun_out/r05_trace/
 #   prof65      the 65B decode under rocprofv3 --kernel-trace         -> gpurun_out/r05_prof65/
 #   ab13        13B Q4_1 decode with and without half-group work units -> gpurun_out/r05_ab13/
+# Probe steps run binaries built beforehand in this container (never on the box):
+#   x: make -C tools/probe mv_probe mv_probe_x;  mmx: make -C tools/probe mm_probe MM_EXPS="...";
+#   trace: make -C tools/probe mv_probe_T;  l2: make -C tools/probe l2_probe;  libab: a library in
+#   llama.vk_amd/lib/ab_base.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
