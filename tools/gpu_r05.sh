@@ -12,6 +12,13 @@
 #   trace       per-wave phase stamps of the Wo / W2 decode matvecs   -> gpurun_out/r05_trace/
 #   prof65      the 65B decode under rocprofv3 --kernel-trace         -> gpurun_out/r05_prof65/
 #   ab13        13B Q4_1 decode with and without half-group work units -> gpurun_out/r05_ab13/
+#   smoke       __graft_entry__.smoke()                               -> gpurun_out/r05_smoke.log
+#   diag7       the 7B bench under rocprofv3 with the fault dump (DIAG_ENV: extra environment)
+#   x / mmx     decode / prompt matmul knockout probes                -> gpurun_out/r05_x/, r05_mmx/
+#   mmab        prompt matmul probe builds A/B (MMB)                  -> gpurun_out/r05_mmab/
+#   envab       one environment switch A/B on the 7B bench legs (ABVAR, ABVALS, ABTESTS)
+#   libab       library A/B (lib/ab_base vs the tree) on decode_speed (ABMODEL, ABTESTS)
+#   ab41        Q4_1 in-kernel weight sums A/B (LVK_MV41_WSI; the variant is removed since)
 # Probe steps run binaries built beforehand in this container (never on the box):
 #   x: make -C tools/probe mv_probe mv_probe_x;  mmx: make -C tools/probe mm_probe MM_EXPS="...";
 #   trace: make -C tools/probe mv_probe_T;  l2: make -C tools/probe l2_probe;  libab: a library in
