@@ -878,10 +878,30 @@ struct GraphEngine {
         }
         if (m.hip_host == 1) { std::fill(m.valid.begin(), m.valid.end(), 0); return; }
         if (T.ok) {
+            // soft-dirty bits, read per run of pages; runs inside a read-only private mapping are
+            // skipped: without a write permission (a change of it shows in maps_now) the process
+            // cannot have written them, and a 7B / 65B weight mirror is almost all such pages
             std::vector<uint64_t> e;
-            if (!T.read(m.page0(), m.pages(), e)) { std::fill(m.valid.begin(), m.valid.end(), 0); return; }
-            for (size_t i = 0; i < e.size(); ++i)
-                if (DirtyTracker::written(e[i])) m.valid[i] = 0;
+            const size_t np = m.pages();
+            auto it = maps_now.begin();
+            for (size_t i = 0; i < np;) {
+                const uintptr_t a = (m.page0() + i) * PAGE;
+                while (it != maps_now.end() && it->hi <= a) ++it;
+                const bool inside = it != maps_now.end() && a >= it->lo;
+                const uintptr_t lim = it == maps_now.end() ? UINTPTR_MAX : inside ? it->hi : it->lo;
+                size_t j = i + 1;
+                while (j < np && (m.page0() + j) * PAGE < lim) ++j;
+                const bool ro = inside && !strchr(it->perms, 'w') && it->perms[3] == 'p';
+                if (!ro) {
+                    if (!T.read(m.page0() + i, j - i, e)) {
+                        std::fill(m.valid.begin() + i, m.valid.begin() + j, 0);
+                    } else {
+                        for (size_t k = 0; k < e.size(); ++k)
+                            if (DirtyTracker::written(e[k])) m.valid[i + k] = 0;
+                    }
+                }
+                i = j;
+            }
         } else {
             for (size_t i = 0; i < m.valid.size(); ++i)
                 if (m.ro[i] < 0 || !ro_alive[(size_t) m.ro[i]]) m.valid[i] = 0;
