@@ -182,6 +182,16 @@ for step in "$@"; do
           | sed "s/^{/{\"lib_ab\": \"$l\", /" | tee -a $O/ab.jsonl || exit 182
       done
     done ;;
+  pfsweep)
+    # prologue orders (LVK_MV_PF 0..5) of the Q4_0 decode matvecs on the current kernels, sweep probe
+    # build (tools/probe/mv_probe_S, make -C tools/probe mv_probe_S), n_past 256, twice
+    O=gpurun_out/r05_pfsweep; mkdir -p $O
+    for r in 1 2; do
+      for pf in 0 1 2 3 4 5; do
+        LVK_MV_PF=$pf LVK_CFG=0 timeout -k 10 120 ./tools/probe/mv_probe_S 256 > $O/pf${pf}_$r.log 2>&1 || exit 191
+        echo "pf $pf: $(grep -E '^  (qkv|wo|w13|w2|lm_head) ' $O/pf${pf}_$r.log | tr -s ' ' | cut -d' ' -f2,3 | tr '\n' ' ')"
+      done
+    done ;;
   ab13)
     # 13B Q4_1 decode: half-group work units (LVK_MV41_HALF) A/B, twice each
     O=gpurun_out/r05_ab13; mkdir -p $O
