@@ -220,8 +220,10 @@ LVK_API int lvk_stage_link_probe(struct llama_context * ctx, int bytes, int iter
  * lvk_ggml_stats: the last call's out[0] host->device bytes, out[1] device->host bytes (the
  * byte ranges the nodes wrote), out[2] bytes of Q4 weights repacked, out[3] host bytes
  * mirrored in HBM after the call; out[4] the tracking mode (0 off: LVK_GGML_CACHE=0, 1
- * read-only mappings only, 2 soft-dirty pages), out[5] 1 once any graph has run.  Fills
- * min(n, 6) values, returns 6 (-1 on bad arguments).
+ * read-only mappings only: LVK_GGML_CACHE=1 or no soft-dirty bits, 2 soft-dirty pages),
+ * out[5] 1 once any graph has run, out[6] the call's host microseconds of tracking
+ * bookkeeping, out[7] of them the microseconds in clear_refs.  Fills min(n, 8) values,
+ * returns 8 (-1 on bad arguments).
  * lvk_ggml_invalidate: the caller changed [p, p + n) in a way that tracking cannot see
  * (write-enabled a read-only buffer, wrote, protected it again between two calls); its
  * pages are uploaded again by the next call.  0 / -1. */

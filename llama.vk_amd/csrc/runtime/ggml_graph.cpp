@@ -17,6 +17,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cinttypes>
 #include <cmath>
 #include <cstdio>
@@ -615,8 +616,14 @@ size_t span_bytes(const ggml_tensor * t) {
 //     wrote travel back.
 // The soft-dirty bits are per process: before a call clears them, every engine (one per
 // device) folds the bits into the validity of all its mirrors.
-// LVK_GGML_CACHE=0 turns the caching off (every needed page uploaded on every call).
+// LVK_GGML_CACHE=0 turns the caching off (every needed page uploaded on every call);
+// LVK_GGML_CACHE=1 keeps the read-only-mapping rule but no soft-dirty tracking (writable
+// pages uploaded on every call, no clear_refs).
 constexpr size_t PAGE = 4096;
+
+uint64_t ns_since(std::chrono::steady_clock::time_point t0) {
+    return (uint64_t) std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
 
 struct MapEnt {
     uintptr_t lo = 0, hi = 0;
@@ -677,6 +684,7 @@ struct DirtyTracker {
     DirtyTracker() {
         const char * e = getenv("LVK_GGML_CACHE");
         if (e && atoi(e) == 0) { enabled = false; return; }
+        if (e && atoi(e) == 1) return;
         pagemap = open("/proc/self/pagemap", O_RDONLY | O_CLOEXEC);
         clear_refs = open("/proc/self/clear_refs", O_WRONLY | O_CLOEXEC);
         if (pagemap < 0 || clear_refs < 0) return;
@@ -760,6 +768,7 @@ bool overlaps(const char * a0, const char * a1, const char * b0, const char * b1
 
 struct GraphStats {
     uint64_t h2d = 0, d2h = 0, repack = 0, mirrored = 0;
+    uint64_t track_ns = 0, clear_ns = 0;   // host time of the validity bookkeeping / of clear_refs
 };
 
 // the persistent device state of ggml_graph_compute on one device
@@ -1260,8 +1269,10 @@ extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph
             }
         }
         DirtyTracker & T = tracker();
+        const auto t_track0 = std::chrono::steady_clock::now();
         if (T.enabled) R.snapshot_maps();
         for (Mirror * m : R.used) R.refresh_validity(*m);
+        R.last.track_ns += ns_since(t_track0);
         // the bytes a node reads before any earlier node of this call wrote them (leaves, the
         // caller's inputs, a KV cache) are the only ones that must come from the host
         {
@@ -1341,17 +1352,21 @@ extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph
         // the soft-dirty bits are process-wide: every engine's mirrors this call did not use
         // (all those of the other devices' engines) note their host writes before the clear
         if (T.ok) {
+            const auto t_fold0 = std::chrono::steady_clock::now();
             for (auto & kv : all_engines()) {
                 GraphEngine & E = *kv.second;
                 if (&E != &R) E.maps_now = R.maps_now;
                 for (Mirror * m : E.mirrors)
                     if (&E != &R || m->last_call != R.calls) E.refresh_validity(*m);
             }
+            const auto t_clear0 = std::chrono::steady_clock::now();
             if (!T.clear()) {
                 T.ok = false;
                 for (auto & kv : all_engines())
                     for (Mirror * m : kv.second->mirrors) std::fill(m->valid.begin(), m->valid.end(), 0);
             }
+            R.last.clear_ns = ns_since(t_clear0);
+            R.last.track_ns += ns_since(t_fold0);
         }
         uint64_t resident = 0;
         for (Mirror * m : R.mirrors) resident += (uint64_t) (m->hi - m->lo);
@@ -1367,11 +1382,12 @@ extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph
 extern "C" int lvk_ggml_stats(uint64_t * out, int n) {
     std::lock_guard<std::mutex> lock(engine_mutex());
     const DirtyTracker & T = tracker();
-    const uint64_t v[6] = {g_last_stats.h2d, g_last_stats.d2h, g_last_stats.repack, g_last_stats.mirrored,
-                           (uint64_t) (!T.enabled ? 0 : T.ok ? 2 : 1), (uint64_t) (g_have_engine ? 1 : 0)};
+    const uint64_t v[8] = {g_last_stats.h2d, g_last_stats.d2h, g_last_stats.repack, g_last_stats.mirrored,
+                           (uint64_t) (!T.enabled ? 0 : T.ok ? 2 : 1), (uint64_t) (g_have_engine ? 1 : 0),
+                           g_last_stats.track_ns / 1000, g_last_stats.clear_ns / 1000};
     if (!out || n < 0) return -1;
-    for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
-    return 6;
+    for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+    return 8;
 }
 
 // the caller rewrote [p, p + n) in a way the tracking cannot see (see above): upload it again
