@@ -215,12 +215,13 @@ LVK_API int lvk_stage_link_probe(struct llama_context * ctx, int bytes, int iter
 /* ggml_graph_compute keeps the host ranges of its tensors mirrored in HBM across calls and
  * uploads only bytes a node reads before the call writes them, and of those only pages the
  * host may have changed: pages of read-only mappings (a PROT_READ model file, an mprotect'ed
- * buffer) while the mapping is unchanged, writable pages only where the kernel's soft-dirty
- * bits track writes (else on every call).  Q4 weights are repacked once per upload.
+ * buffer) while the mapping is unchanged; writable pages go again on every call unless
+ * LVK_GGML_CACHE=2 tracks them with the kernel's soft-dirty bits (process-wide clear_refs,
+ * opt-in: measured slower in a HIP process).  Q4 weights are repacked once per upload.
  * lvk_ggml_stats: the last call's out[0] host->device bytes, out[1] device->host bytes (the
  * byte ranges the nodes wrote), out[2] bytes of Q4 weights repacked, out[3] host bytes
  * mirrored in HBM after the call; out[4] the tracking mode (0 off: LVK_GGML_CACHE=0, 1
- * read-only mappings only: LVK_GGML_CACHE=1 or no soft-dirty bits, 2 soft-dirty pages),
+ * read-only mappings only: the default, 2 soft-dirty pages: LVK_GGML_CACHE=2),
  * out[5] 1 once any graph has run, out[6] the call's host microseconds of tracking
  * bookkeeping, out[7] of them the microseconds in clear_refs.  Fills min(n, 8) values,
  * returns 8 (-1 on bad arguments).

@@ -603,10 +603,12 @@ size_t span_bytes(const ggml_tensor * t) {
 //     mapping (address range, offset, device, inode, permissions in /proc/self/maps) is
 //     unchanged -- a caller that re-enables writes, writes and protects again between two
 //     calls must say so with lvk_ggml_invalidate;
-//   * writable pages are tracked by the kernel's soft-dirty bits where they work
-//     (/proc/self/pagemap bit 55, cleared by "4" into /proc/self/clear_refs; a new mapping
-//     reads dirty, a page that is neither present nor swapped counts as written), and are
-//     uploaded again on every call where they do not;
+//   * writable pages are uploaded again on every call.  LVK_GGML_CACHE=2 tracks them with
+//     the kernel's soft-dirty bits instead (/proc/self/pagemap bit 55, cleared by "4" into
+//     /proc/self/clear_refs; a new mapping reads dirty, a page that is neither present nor
+//     swapped counts as written).  That is opt-in: the clear is process-wide, and in a HIP
+//     process the call after it stalls for ~0.2 s (tools/ggml_graph/track_cost.c, DESIGN.md
+//     section 5), more than re-uploading gigabytes of writable pages costs;
 //   * pages the CPU-side tracking cannot see written are never kept: pages of shared mappings
 //     (another mapping or process may write them; HIP's pinned host allocations are shared
 //     mappings of the driver's device file) and host memory registered with HIP (a DMA into
@@ -616,9 +618,8 @@ size_t span_bytes(const ggml_tensor * t) {
 //     wrote travel back.
 // The soft-dirty bits are per process: before a call clears them, every engine (one per
 // device) folds the bits into the validity of all its mirrors.
-// LVK_GGML_CACHE=0 turns the caching off (every needed page uploaded on every call);
-// LVK_GGML_CACHE=1 keeps the read-only-mapping rule but no soft-dirty tracking (writable
-// pages uploaded on every call, no clear_refs).
+// LVK_GGML_CACHE=0 turns the caching off (every needed page uploaded on every call); 1 (the
+// default) keeps pages of read-only mappings; 2 adds the soft-dirty tracking of writable pages.
 constexpr size_t PAGE = 4096;
 
 uint64_t ns_since(std::chrono::steady_clock::time_point t0) {
@@ -662,7 +663,7 @@ const MapEnt * map_of(const std::vector<MapEnt> & v, uintptr_t a) {
 struct DirtyTracker {
     int pagemap = -1, clear_refs = -1;
     bool enabled = true;       // LVK_GGML_CACHE != 0
-    bool ok = false;           // soft-dirty bits work
+    bool ok = false;           // LVK_GGML_CACHE=2 and the soft-dirty bits work
 
     bool read(uintptr_t page0, size_t n, std::vector<uint64_t> & e) const {
         e.resize(n);
@@ -683,8 +684,9 @@ struct DirtyTracker {
 
     DirtyTracker() {
         const char * e = getenv("LVK_GGML_CACHE");
-        if (e && atoi(e) == 0) { enabled = false; return; }
-        if (e && atoi(e) == 1) return;
+        const int mode = e ? atoi(e) : 1;
+        if (mode == 0) { enabled = false; return; }
+        if (mode != 2) return;
         pagemap = open("/proc/self/pagemap", O_RDONLY | O_CLOEXEC);
         clear_refs = open("/proc/self/clear_refs", O_WRONLY | O_CLOEXEC);
         if (pagemap < 0 || clear_refs < 0) return;

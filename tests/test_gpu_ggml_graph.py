@@ -37,8 +37,9 @@ def test_graph_compute_matches_reference_ggml(gpu_available, wtype, kv, tmp_path
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cache", ["1", "2"])
 @pytest.mark.parametrize("wtype", [0, 1])
-def test_graph_compute_uploads_weights_once(gpu_available, wtype, tmp_path):
+def test_graph_compute_uploads_weights_once(gpu_available, wtype, cache, tmp_path):
     """ggml_graph_compute keeps its device state across calls: the weights (a read-only
     buffer of the caller, like llama.cpp's PROT_READ model mapping) go host -> device and
     are repacked in the first call only; each later decode step uploads just what the host
@@ -46,7 +47,7 @@ def test_graph_compute_uploads_weights_once(gpu_available, wtype, tmp_path):
     bytes) and copies back just the bytes its nodes wrote.  The logits of the compared
     steps stay those of the plain run (test above)."""
     _build()
-    env = dict(os.environ, GRAPH_TEST_REPEAT="6")
+    env = dict(os.environ, GRAPH_TEST_REPEAT="6", LVK_GGML_CACHE=cache)
     r = subprocess.run([LVK_BIN, str(tmp_path / "x.bin"), str(wtype), "1"], capture_output=True, text=True,
                        env=env, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -64,19 +65,22 @@ def test_graph_compute_uploads_weights_once(gpu_available, wtype, tmp_path):
         assert c["repack"] == 0, calls
         assert c["h2d"] < wbytes / 4, calls
         assert c["d2h"] < wbytes / 4, calls
-        assert c["mode"] in (1, 2), calls
+        assert c["mode"] == int(cache), calls
     print("per-call ms:", [round(c["ms"], 3) for c in calls], "h2d:", [int(c["h2d"]) for c in calls])
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cache", ["1", "2"])
 @pytest.mark.parametrize("mode", ["private", "pinned", "shared"])
-def test_graph_compute_sees_untracked_host_writes(gpu_available, mode):
+def test_graph_compute_sees_untracked_host_writes(gpu_available, mode, cache):
     """the mirrors must not keep a stale device copy of host bytes that change where the CPU
     page tables cannot see it between two calls: a hipMemcpy D2H (DMA) into a pinned context
-    buffer, a write through a second MAP_SHARED view of the buffer's pages, and (the tracked
-    case) a plain CPU write (tools/ggml_graph/volatile_test.cpp: z = x + y checked after each)"""
+    buffer, a write through a second MAP_SHARED view of the buffer's pages, and a plain CPU
+    write (tools/ggml_graph/volatile_test.cpp: z = x + y checked after each); under the
+    default caching (1) and under the opt-in soft-dirty tracking of writable pages (2)"""
     b = os.path.join(os.path.dirname(LVK_BIN), "volatile_test")
     if not os.path.exists(b):
         subprocess.check_call(["make", "-C", os.path.dirname(os.path.dirname(b))], stdout=subprocess.DEVNULL)
-    r = subprocess.run([b, mode], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([b, mode], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, LVK_GGML_CACHE=cache))
     assert r.returncode == 0 and ("ok %s" % mode) in r.stdout, r.stderr[-2000:]
