@@ -111,6 +111,30 @@ __device__ __forceinline__ double warp_sum_d(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
+
+// ggml_compute_forward_rms_norm_f32 (ggml.c:6060-6065) adds the float squares x[i] * x[i] to a
+// double in index order; the kernels add the same terms as a tree.  For n nonnegative terms
+// either order lies within (n - 1)u of the exact sum (u = 2^-53), so the two sums differ by at
+// most 2(n - 1)u of it, and (float)(sum / n) -- both roundings monotone -- is the same for both
+// unless a float rounding boundary lies that close to sum / n.  rms_mean returns the tree's mean
+// when the nearest boundary is farther than 4nu (twice the bound), else (about one row in 1e5)
+// the mean of an index-order re-sum of the row x[0 .. n): the reference's float mean either way.
+// the cold path of rms_mean: out of line, so that its loop adds no registers to the kernels
+__device__ __noinline__ float rms_mean_in_order(const float * x, int n) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) { const float v = x[i]; const float sq = v * v; s += (double) sq; }
+    return (float) (s / (double) n);
+}
+__device__ __forceinline__ float rms_mean(double tree, const float * x, int n) {
+    const double r = tree / (double) n;
+    const float f = (float) r;
+    const uint32_t b = __float_as_uint(f);
+    const double up = 0.5 * ((double) f + (double) __uint_as_float(b + 1u));
+    const double dn = 0.5 * ((double) f + (b ? (double) __uint_as_float(b - 1u) : -(double) __uint_as_float(1u)));
+    const double slack = r * ((double) n * 0x1p-51);
+    if (r + slack < up && r - slack > dn) return f;
+    return rms_mean_in_order(x, n);
+}
 // whole-wave double sum through DPP (quad xor 1, xor 2, half-row and row
 // mirrors) and four readlanes; every lane returns the same value, and the
 // association order is fixed: ((row0 + row1) + (row2 + row3)) of 16-lane trees

@@ -58,9 +58,8 @@ struct Params {
 // ---------------------------------------------------------------------------
 // Prologue A (PRO_NORM): x[t] -> rms_norm -> * g -> quantize_row_q4_0, into
 // the LDS table.  ggml.c:6058-6076 then llama.cpp:984.  The double sum of
-// squares is reduced as a tree: every term is a float square carried exactly
-// in double, so the float mean equals the sequential reference except when the
-// sum sits within ~1e-13 relative of a float rounding boundary.
+// squares is reduced as a tree; rms_mean (lvk_device.h) returns the index-order
+// mean (a re-sum when the tree's lies near a float rounding boundary).
 // Work unit = 8 consecutive elements; a block's 4 units are a thread quad.
 // ---------------------------------------------------------------------------
 template <int NT, int T, int UMAX, bool PRE>
@@ -103,7 +102,8 @@ __device__ void prologue_norm(const Params & P, int t0, int nt, uint32_t * act_b
     if (tid < T) {
         double s = 0.0;
         for (int w = 0; w < NT / 64; ++w) s += red[tid * (NT / 64) + w];
-        const float mean = (float) (s / (double) K);
+        // rows tid >= nt summed nothing: s == 0 never re-reads x
+        const float mean = rms_mean(s, P.x + (size_t) (P.tok0 + t0 + tid) * K, K);
         s_scale[tid] = 1.0f / sqrtf(mean + 1e-6f);
     }
     __syncthreads();

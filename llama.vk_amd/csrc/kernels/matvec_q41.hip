@@ -112,7 +112,8 @@ __global__ __launch_bounds__(NT) void k_matvec_q41(P41 P) {
             if (tid < T) {
                 double s = 0.0;
                 for (int w = 0; w < NW; ++w) s += red[tid * NW + w];
-                const float mean = (float) (s / (double) K);
+                // rows tid >= nt summed nothing: s == 0 never re-reads x
+                const float mean = rms_mean(s, P.x + (size_t) (P.tok0 + t0 + tid) * K, K);
                 s_scale[tid] = 1.0f / sqrtf(mean + 1e-6f);
             }
             __syncthreads();

@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256) void k_act_q41_f16(const float * __restrict__ 
         if (tid == 0) {
             double s = 0.0;
             for (int wv = 0; wv < 4; ++wv) s += red[wv];
-            const float mean = (float) (s / (double) K);          // ggml.c:6058-6071
+            const float mean = rms_mean(s, xr, K);                // ggml.c:6058-6071
             s_scale = 1.0f / sqrtf(mean + 1e-6f);
         }
         __syncthreads();

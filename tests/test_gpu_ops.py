@@ -281,3 +281,80 @@ def test_ggml_internal_get_quantize_fn_vs_reference_build(lvk, ref):
         w = ref.quantize((rng.standard_normal(4096) * 0.4).astype(np.float32), qt)
         assert np.float32(f.vec_dot(4096, w, q)).view(np.uint32) == np.float32(ref.vec_dot(qt, 4096, w, q)).view(np.uint32)
     assert not lvk.QuantizeFns(6).valid          # GGML_TYPE_F32: no codec entry
+
+
+# ---------------------------------------------------------------------------
+# RMSNorm rows whose float mean depends on the summation order (RMSNorm
+# order; lvk_device.h rms_mean).  x[0]^2 + x[1]^2 puts sum / K exactly on a float rounding
+# midpoint, and each of the K - 2 equal tiny squares is below half an ulp of that sum: the
+# reference's index-order double sum (ggml.c:6060-6065) drops them all and the tie rounds to
+# even, while a tree that adds the tiny terms first keeps them and rounds up.  Found by a
+# seeded search over 12-bit x[0], x[1] (tests/golden/make_rms_order_rows.py).
+# ---------------------------------------------------------------------------
+_RMS_ORDER_ROWS = {
+    256: (1.1416015625, 0.574951171875, 7.450580596923828e-09),
+    4096: (0.95947265625, 0.394775390625, 7.450580596923828e-09),
+    5120: (17.3515625, 4.544921875, 1.1920928955078125e-07),
+}
+
+
+def _rms_order_rows(rng, k, n, scale=1.0):
+    """n rows: even rows are the order-sensitive row (times a power of two), odd rows random"""
+    a, b, t = _RMS_ORDER_ROWS[k]
+    x = (rng.standard_normal((n, k)) * 1.3).astype(np.float32)
+    for i in range(0, n, 2):
+        x[i] = np.float32(t)
+        x[i, 0], x[i, 1] = a, b
+        x[i] *= np.float32(scale * 2.0 ** (i % 3))
+    return x
+
+
+def _rms_exact_sum(x, g):
+    """g * rms_norm(x) with the exactly rounded sum of squares (what a tree that keeps every
+    tiny term gives here) instead of the index-order one"""
+    import math
+    out = np.empty_like(x)
+    k = x.shape[1]
+    for i, row in enumerate(x):
+        sq = (row * row).astype(np.float32)
+        mean = np.float32(math.fsum(float(v) for v in sq) / k)
+        sc = np.float32(1.0) / np.sqrt(np.float32(mean + np.float32(1e-6)), dtype=np.float32)
+        out[i] = g * (row * sc).astype(np.float32)
+    return out.astype(np.float32)
+
+
+def _rms_oracle(oracle, x, g):
+    n, k = x.shape
+    xn = np.zeros_like(x)
+    oracle.lib.orc_rms_norm(np.ascontiguousarray(x), k, n, xn)
+    return (g[None, :] * xn).astype(np.float32)
+
+
+def test_rms_norm_order_sensitive_rows_vs_oracle(lvk, oracle):
+    """the row helper of the embeddings path (k_rmsnorm_rows): the index-order mean"""
+    rng = np.random.default_rng(61)
+    x = _rms_order_rows(rng, 4096, 4)
+    g = (1 + 0.1 * rng.standard_normal(4096)).astype(np.float32)
+    want = _rms_oracle(oracle, x, g)
+    assert not np.array_equal(bits(want[0]), bits(_rms_exact_sum(x[:1], g)[0])), "row not order-sensitive"
+    assert np.array_equal(bits(lvk.rms_norm_mul(x, g)), bits(want))
+
+
+@pytest.mark.parametrize("qt,k,n,mfma", [(2, 4096, 1, False), (2, 4096, 5, False), (2, 256, 1, False),
+                                         (2, 4096, 17, True), (3, 5120, 1, False), (3, 5120, 3, False),
+                                         (3, 5120, 17, True), (3, 256, 1, False)])
+def test_rmsnorm_prologues_order_sensitive_rows(lvk, oracle, qt, k, n, mfma):
+    """every fused RMSNorm prologue -- decode matvecs (k_mv_cu / k_mv_cu41), batched matvecs
+    (k_matvec_q40 / q41) and the prompt activation kernels (k_act_q40_f16 / q41) -- on rows
+    whose mean the summation order changes: the products equal the oracle's, which follows
+    the reference's index order, and differ from what the exactly rounded sum would give"""
+    rng = np.random.default_rng(qt * 100 + k + n)
+    m = 128
+    wq = _weights(oracle, rng, m, k, qt)
+    x = _rms_order_rows(rng, k, n)
+    g = (1.0 + 0.1 * rng.standard_normal(k)).astype(np.float32)
+    want = _oracle_mm(oracle, wq, [oracle.quantize(r, qt) for r in _rms_oracle(oracle, x, g)], k, qt)
+    other = _oracle_mm(oracle, wq, [oracle.quantize(r, qt) for r in _rms_exact_sum(x, g)], k, qt)
+    assert not np.array_equal(bits(want[0]), bits(other[0])), "row 0 not order-sensitive through the matvec"
+    got = lvk.mul_mat_q_mfma(qt, wq, m, k, x, g=g) if mfma else lvk.mul_mat_q_norm(qt, wq, m, k, g, x)
+    assert np.array_equal(bits(got), bits(want))
