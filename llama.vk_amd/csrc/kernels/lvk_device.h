@@ -114,12 +114,13 @@ __device__ __forceinline__ double warp_sum_d(double v) {
 
 // ggml_compute_forward_rms_norm_f32 (ggml.c:6060-6065) adds the float squares x[i] * x[i] to a
 // double in index order; the kernels add the same terms as a tree.  For n nonnegative terms
-// either order lies within (n - 1)u of the exact sum (u = 2^-53), so the two sums differ by at
-// most 2(n - 1)u of it, and (float)(sum / n) -- both roundings monotone -- is the same for both
-// unless a float rounding boundary lies that close to sum / n.  rms_mean returns the tree's mean
-// when the nearest boundary is farther than 4nu (twice the bound), else (about one row in 1e5)
-// the mean of an index-order re-sum of the row x[0 .. n): the reference's float mean either way.
-// the cold path of rms_mean: out of line, so that its loop adds no registers to the kernels
+// either order lies within (n - 1)u of the exact sum (u = 2^-53), so the two means sum / n (one
+// more rounding each) differ by at most 2n ulps of the double r = sum / n.  (float) r rounds on
+// the 29 double significand bits below the float's; its only rounding boundary is the midpoint
+// pattern 2^28.  rms_mean keeps the tree's mean when those bits are more than 4n from the
+// midpoint (r a normal float, or 0), else (about one row in 1e5) it returns the mean of an
+// index-order re-sum of x[0 .. n): the reference's float mean either way.
+// The cold path is out of line, so that its loop adds no registers to the kernels.
 __device__ __noinline__ float rms_mean_in_order(const float * x, int n) {
     double s = 0.0;
     for (int i = 0; i < n; ++i) { const float v = x[i]; const float sq = v * v; s += (double) sq; }
@@ -127,12 +128,11 @@ __device__ __noinline__ float rms_mean_in_order(const float * x, int n) {
 }
 __device__ __forceinline__ float rms_mean(double tree, const float * x, int n) {
     const double r = tree / (double) n;
-    const float f = (float) r;
-    const uint32_t b = __float_as_uint(f);
-    const double up = 0.5 * ((double) f + (double) __uint_as_float(b + 1u));
-    const double dn = 0.5 * ((double) f + (b ? (double) __uint_as_float(b - 1u) : -(double) __uint_as_float(1u)));
-    const double slack = r * ((double) n * 0x1p-51);
-    if (r + slack < up && r - slack > dn) return f;
+    const uint64_t rb = (uint64_t) __double_as_longlong(r);
+    const uint32_t ex = (uint32_t) (rb >> 52);                  // r >= 0: no sign bit
+    const int32_t mid = (int32_t) (uint32_t) (rb & 0x1fffffffu) - (1 << 28);
+    const bool safe = rb == 0 || (ex >= 1023 - 126 && ex < 1023 + 128 && (mid > 4 * n || mid < -4 * n));
+    if (__builtin_expect(safe, 1)) return (float) r;
     return rms_mean_in_order(x, n);
 }
 // whole-wave double sum through DPP (quad xor 1, xor 2, half-row and row
