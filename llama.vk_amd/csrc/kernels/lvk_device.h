@@ -135,6 +135,33 @@ __device__ __forceinline__ float rms_mean(double tree, const float * x, int n) {
     if (__builtin_expect(safe, 1)) return (float) r;
     return rms_mean_in_order(x, n);
 }
+// rms_mean for a call made by all 64 lanes of a wave with the same arguments.  Before the
+// index-order re-sum it tries an exactness certificate, split over the lanes: when every square
+// is a multiple of 2^m and the sum is below 2^(m+53), every partial sum in any order is exact,
+// so the tree's sum is the index-order one.  The synthetic models' activations carry few
+// significant bits and often sit exactly on a midpoint, and this certificate covers them.
+__device__ __forceinline__ float rms_mean_wave(double tree, const float * x, int n) {
+    const double r = tree / (double) n;
+    const uint64_t rb = (uint64_t) __double_as_longlong(r);
+    const uint32_t ex = (uint32_t) (rb >> 52);
+    const int32_t mid = (int32_t) (uint32_t) (rb & 0x1fffffffu) - (1 << 28);
+    const bool safe = rb == 0 || (ex >= 1023 - 126 && ex < 1023 + 128 && (mid > 4 * n || mid < -4 * n));
+    if (__builtin_expect(safe, 1)) return (float) r;
+    int mlow = 1 << 20;            // lowest set-bit exponent over the nonzero squares
+    for (int i = (int) (threadIdx.x & 63); i < n; i += 64) {
+        const float v = x[i];
+        const float sq = v * v;
+        const uint32_t b = __float_as_uint(sq);
+        if (b != 0u) {
+            const uint32_t e = b >> 23, man = (b & 0x7fffffu) | (e ? 0x800000u : 0u);
+            const int low = (e ? (int) e - 150 : -149) + __builtin_ctz(man);
+            mlow = low < mlow ? low : mlow;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) { const int t = __shfl_xor(mlow, o); mlow = t < mlow ? t : mlow; }
+    if (mlow == (1 << 20) || tree <= ldexp(1.0, mlow + 52)) return (float) r;
+    return rms_mean_in_order(x, n);
+}
 // whole-wave double sum through DPP (quad xor 1, xor 2, half-row and row
 // mirrors) and four readlanes; every lane returns the same value, and the
 // association order is fixed: ((row0 + row1) + (row2 + row3)) of 16-lane trees

@@ -126,7 +126,7 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
                 }
                 LVK_T(56);
                 acc = warp_sum_d(acc);
-                const float mean = rms_mean(acc, P.x, KT);
+                const float mean = rms_mean_wave(acc, P.x, KT);
                 scale = 1.0f / sqrtf(mean + 1e-6f);
                 LVK_T(57);
             }
@@ -304,7 +304,7 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
                 LVK_T(60);
                 double sum = red[0];
                 for (int w = 1; w < NW; ++w) sum += red[w];
-                const float mean = rms_mean(sum, P.x, KT);
+                const float mean = rms_mean_wave(sum, P.x, KT);
                 scale = 1.0f / sqrtf(mean + 1e-6f);
             }
 #pragma unroll

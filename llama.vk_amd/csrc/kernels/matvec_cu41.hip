@@ -187,7 +187,7 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
             __syncthreads();
             double sum = red[0];
             for (int w = 1; w < NW; ++w) sum += red[w];
-            const float mean = rms_mean(sum, P.x, KT);
+            const float mean = rms_mean_wave(sum, P.x, KT);
             scale = 1.0f / sqrtf(mean + 1e-6f);
         }
 #pragma unroll

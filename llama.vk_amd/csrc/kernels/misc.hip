@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void k_rmsnorm_rows(const float * __restrict__
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
     const double s = (red[0] + red[1]) + (red[2] + red[3]);
-    const float mean = rms_mean(s, xr, K);
+    const float mean = rms_mean_wave(s, xr, K);
     const float scale = 1.0f / sqrtf(mean + 1e-6f);
     for (int i = threadIdx.x; i < K; i += 256) { const float yn = xr[i] * scale; y[(size_t) t * K + i] = g[i] * yn; }
 }

@@ -503,11 +503,11 @@ __global__ __launch_bounds__(256) void k_act_q40_f16(const float * __restrict__ 
         acc = warp_sum_d(acc);
         if ((tid & 63) == 0) red[tid >> 6] = acc;
         __syncthreads();
-        if (tid == 0) {
+        if (tid < 64) {             // wave 0: rms_mean_wave splits a re-check over its lanes
             double s = 0.0;
             for (int wv = 0; wv < 4; ++wv) s += red[wv];
-            const float mean = rms_mean(s, xr, K);                // ggml.c:6058-6071
-            s_scale = 1.0f / sqrtf(mean + 1e-6f);
+            const float mean = rms_mean_wave(s, xr, K);           // ggml.c:6058-6071
+            if (tid == 0) s_scale = 1.0f / sqrtf(mean + 1e-6f);
         }
         __syncthreads();
         scale = s_scale;
