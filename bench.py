@@ -516,14 +516,13 @@ def decode_65b(args, coord, n_ctx, ptoks):
     t0 = time.time()
     m = lvk.Llama(path, n_ctx=n_ctx)
     load_s = time.time() - t0
-    lg = m.eval(ptoks, 0)
-    tok = int(np.argmax(lg[-1]))
-    for i in range(4):
-        tok = int(np.argmax(m.eval([tok], 16 + i)[-1]))
+    # the window is filled once (every K / V row exists), then the timed steps are spread
+    # evenly over positions 16..n_ctx-1, as in the 7B line
+    tok = fill_window(m, ptoks, n_ctx)
     coord.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps_65b):
-        tok = int(np.argmax(m.eval([tok], 16 + (i % (n_ctx - 16)))[-1]))
+        tok = int(np.argmax(m.eval([tok], spread_pos(i, args.steps_65b, n_ctx), copy=False)[-1]))
     dt = coord.max(time.perf_counter() - t0)
     r = args.steps_65b / dt
     m.set_profiling(True)
@@ -532,13 +531,9 @@ def decode_65b(args, coord, n_ctx, ptoks):
         tok = int(np.argmax(m.eval([tok], 16 + i * 60)[-1]))
     prof = m.profile()
     m.set_profiling(False)
-    # the greedy steps a layer split's stages run (layer_split's greedy_check): 16-token
-    # prompt, then SPLIT_FIRST_TOKEN at n_past 16, ...
-    m.eval(ptoks, 0)
-    tok, check = SPLIT_FIRST_TOKEN, []
-    for i in range(16):
-        tok = m.eval_greedy(tok, 16 + i)
-        check.append(tok)
+    # teacher-forced stream check (a synthetic model's greedy stream repeats one token): the
+    # chained device decode must reproduce every per-step llama_eval logits digest
+    stream = stream_check(m, ptoks, args.stream_check_65b)
     # 1-GPU 65B 512-token prompt (best of 2): the S = 1 reference point of the split's prefill
     ptoks512 = np.array([1] + [100 + (i * 7919) % 31000 for i in range(1, n_ctx)], np.int32)
     best = 1e30
@@ -547,6 +542,7 @@ def decode_65b(args, coord, n_ctx, ptoks):
         t0 = time.perf_counter()
         m.eval(ptoks512, 0)
         best = min(best, coord.max(time.perf_counter() - t0))
+    prompt_image = m.prompt_image_bytes()
     m.close()
     cpu65 = None
     if coord.rank == 0 and coord.ws == 1 and not args.no_cpu_baseline:
@@ -554,6 +550,7 @@ def decode_65b(args, coord, n_ctx, ptoks):
         cpu65 = cpu_baseline(path, args.cpu_budget, label="65B Q4_0", prompt=False, seg_steps=2, n_seg=2)
     fmas = 80 * (4 * 8192 * 8192 + 3 * 8192 * 22016) / 4 * len(ptoks512)
     prompt = {"value": len(ptoks512) / best, "unit": "tok/s", "n_tokens": len(ptoks512), "ms": best * 1e3,
+              "a16_image_bytes": prompt_image,
               "roofline": {"bound": "valu-fp32 (the reference's sequential fp32 FMA chains)",
                            "achieved": 2 * fmas / best / 1e12, "peak": VALU_FP32_TFLOPS, "unit": "TFLOP/s",
                            "frac": 2 * fmas / best / 1e12 / VALU_FP32_TFLOPS, "fp32_chain_fmas": fmas}}
@@ -562,13 +559,13 @@ def decode_65b(args, coord, n_ctx, ptoks):
                for k, v in prof.items() if v["launches"]}
     return {"value": r, "unit": "tok/s", "steps": args.steps_65b, "ms_per_token": 1e3 / r, "prompt_eval": prompt,
             "workload": "LLaMA-65B Q4_0 (synthetic, seed 3; n_embd 8192, 64 heads, 80 layers, n_ff 22016) "
-                        "single-stream greedy decode on 1 GPU, positions 16..%d, n_ctx %d"
-                        % (16 + min(args.steps_65b, n_ctx - 16) - 1, n_ctx),
+                        "single-stream greedy decode on 1 GPU, %d steps at positions spread evenly over "
+                        "16..%d (window filled first), n_ctx %d" % (args.steps_65b, n_ctx - 1, n_ctx),
             "model_bytes_per_token": MODEL_BYTES_65B,
             "frac_hbm_roofline": r * MODEL_BYTES_65B / 1e9 / HBM_PEAK_GBS,
             "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_65B,
             "kernels": kernels, "gen_s": gen_s, "load_s": load_s, "cpu_baseline": cpu65,
-            "greedy_check_tokens": check,
+            "stream_check": stream,
             "vs_cpu_baseline": (r / cpu65["value"]) if cpu65 else None}
 
 
@@ -596,6 +593,8 @@ def main():
                          "shared-memory ring (ranks may share a GPU: the one-GPU rehearsal)")
     ap.add_argument("--stream-check", type=int, default=64,
                     help="teacher-forced steps whose per-step logits digests the chained path must reproduce")
+    ap.add_argument("--stream-check-13b", type=int, default=32)
+    ap.add_argument("--stream-check-65b", type=int, default=16)
     ap.add_argument("--split-check", type=int, default=16,
                     help="greedy steps of the split replayed on one unsplit context by rank 0 (0: none)")
     ap.add_argument("--split-rehearse", action="store_true",
@@ -622,6 +621,9 @@ def main():
         sys.exit(serve_worker(sys.argv[1:]))
     out = run(args, LocalCoord())
     print(json.dumps(out))
+    if out and not out.get("checks", {}).get("passed", True):
+        sys.stderr.write("bench: correctness checks failed: %s\n" % out["checks"]["failed"])
+        sys.exit(1)
 
 
 def run(args, coord):
@@ -683,7 +685,7 @@ def run(args, coord):
     elapsed = coord.max(t1 - t0)
     value = n_gpus * args.steps / elapsed
     positions = ("16..511, each once in order" if args.steps == win else
-                 "%d positions spread evenly over 16..511 (window filled first)" % args.steps if args.steps < win else
+                 "spread evenly over 16..511 (window filled first)" if args.steps < win else
                  "16..511 wrapping to 16 after 511")
 
     greedy = None
@@ -730,16 +732,7 @@ def run(args, coord):
         # the check above passes under many numeric errors): seeded non-repeating tokens through
         # per-step llama_eval and through lvk_decode_chain; every step's device logits digest must
         # equal the digest of the per-step logits row
-        from oracle_lib import forced_tokens
-        seq_f = forced_tokens(args.stream_check)
-        m.eval(ptoks, 0)
-        want = [lvk.logits_digest(m.eval([int(t)], 16 + i)[-1]) for i, t in enumerate(seq_f)]
-        m.eval(ptoks, 0)
-        _, got = m.decode_chain(seq_f, 16)
-        greedy["stream_check"] = {"steps": len(seq_f), "positions": "16..%d" % (15 + len(seq_f)),
-                                  "tokens": "oracle_lib.forced_tokens (seeded, non-repeating)",
-                                  "digests_equal": got.tolist() == want,
-                                  "first_digests": [hex(d) for d in want[:3]]}
+        greedy["stream_check"] = stream_check(m, ptoks, args.stream_check)
         # host sampler (llama_sample_top_p_top_k, main's defaults: top_k 40, top_p 0.95, temp 0.8,
         # repeat_penalty 1.1 over a 64-token window) on fresh logits (lvk_eval_greedy leaves none)
         m.eval([tok], 16)
@@ -783,6 +776,7 @@ def run(args, coord):
     fmas = 512 * LAYER_MAT_WEIGHTS_7B / 4
     macs = 512 * LAYER_MAT_WEIGHTS_7B
     prompt = {"value": n_gpus * 512 / best, "unit": "tok/s", "n_tokens": 512, "ms": best * 1e3,
+              "a16_image_bytes": m.prompt_image_bytes(),
               "path": "matrix cores (v_mfma_f32_32x32x8_f16 exact 4-element integer partials, f32 MFMA scale "
                       "products) + VALU fp32 chains; bit-identical to the AVX2 reference",
               "roofline": {"bound": "valu-fp32 (the reference's sequential fp32 FMA chains)",
@@ -838,17 +832,15 @@ def run(args, coord):
         path13 = os.path.join(os.path.dirname(args.model), "llama-13b-q4_1.bin")
         ensure_model(path13, coord, dict(n_embd=5120, n_head=40, n_layer=40, ftype=3, seed=2))
         m13 = lvk.Llama(path13, n_ctx=n_ctx)
-        lg = m13.eval(ptoks, 0)
-        tok = int(np.argmax(lg[-1]))
-        for i in range(4):
-            lg = m13.eval([tok], 16 + i)
-            tok = int(np.argmax(lg[-1]))
+        tok = fill_window(m13, ptoks, n_ctx)
         coord.barrier()
         t0 = time.perf_counter()
         for i in range(args.steps_13b):
-            lg = m13.eval([tok], 16 + (i % (n_ctx - 16)))
+            lg = m13.eval([tok], spread_pos(i, args.steps_13b, n_ctx), copy=False)
             tok = int(np.argmax(lg[-1]))
         t13 = coord.max(time.perf_counter() - t0)
+        stream13 = stream_check(m13, ptoks, args.stream_check_13b)
+        image13 = m13.prompt_image_bytes()
         # per-kernel-class HIP-event pass (the Q4_1 decode kernels, matvec_cu41.hip)
         m13.set_profiling(True)
         m13.reset_profile()
@@ -869,7 +861,7 @@ def run(args, coord):
         E13, F13 = 5120, 13824
         fmas13 = 2.0 * 40 * (4 * E13 * E13 + 3 * E13 * F13) / 4 * len(ptoks13)   # 16 chain FMAs per 32 weights
         prompt13 = {"value": n_gpus * len(ptoks13) / best13, "unit": "tok/s", "n_tokens": len(ptoks13),
-                    "ms": best13 * 1e3,
+                    "ms": best13 * 1e3, "a16_image_bytes": image13,
                     "path": "matrix cores (chain partials, cross-term sums, scale products) + VALU fp32 chains "
                             "(ggml_vec_dot_q4_1); bit-identical to the AVX2 reference",
                     "roofline": {"bound": "valu-fp32 (the reference's sequential fp32 FMA chains)",
@@ -881,7 +873,9 @@ def run(args, coord):
                for k, v in p13.items() if v["launches"]}
         r13 = args.steps_13b / t13
         q41 = {"value": n_gpus * r13, "unit": "tok/s", "steps": args.steps_13b,
-               "workload": "LLaMA-13B Q4_1 (synthetic, seed 2) single-stream greedy decode, positions 16.., n_ctx 512",
+               "workload": "LLaMA-13B Q4_1 (synthetic, seed 2) single-stream greedy decode, %d steps at positions "
+                           "spread evenly over 16..%d (window filled first), n_ctx %d" % (args.steps_13b, n_ctx - 1, n_ctx),
+               "stream_check": stream13,
                "model_bytes_per_token": MODEL_BYTES_13B_Q41,
                "frac_hbm_roofline": r13 * MODEL_BYTES_13B_Q41 / 1e9 / HBM_PEAK_GBS,
                "roofline_tok_s": HBM_PEAK_GBS * 1e9 / MODEL_BYTES_13B_Q41, "kernels": k13,
@@ -930,7 +924,63 @@ def run(args, coord):
         "cpu_baseline": cpu,
         "load_s": load_s,
     }
+    out["checks"] = collect_checks(out)
     return out
+
+
+def collect_checks(out):
+    """every correctness field the legs recorded: a false one marks the line invalid (bench.py
+    exits non-zero after printing it)"""
+    failed = []
+
+    def walk(node, path):
+        if isinstance(node, dict):
+            for k, v in node.items():
+                if k in CHECK_KEYS and v is not True:
+                    failed.append(path + k)
+                walk(v, path + k + ".")
+
+    walk(out, "")
+    return {"passed": not failed, "failed": failed, "keys": sorted(CHECK_KEYS)}
+
+
+CHECK_KEYS = {"digests_equal", "tokens_match_eval_greedy", "logits_bit_identical_every_step", "match",
+              "prompt_logits_bit_identical", "tokens_equal"}
+
+
+def fill_window(m, ptoks, n_ctx):
+    """16-token prompt, then greedy steps over positions 16..n_ctx-1 (every K / V row of the
+    window exists before a timed step reads it); returns the greedy token after the prompt"""
+    import numpy as np
+    tok = int(np.argmax(m.eval(ptoks, 0)[-1]))
+    for p in range(len(ptoks), n_ctx):
+        tok = int(np.argmax(m.eval([tok], p, copy=False)[-1]))
+    return int(np.argmax(m.eval(ptoks, 0)[-1]))
+
+
+def spread_pos(i, steps, n_ctx, first=16):
+    """position of timed step i: K steps spread evenly over first..n_ctx-1 (K = the window: each
+    once, in order; more: wrapping)"""
+    win = n_ctx - first
+    return first + (i * win // steps if steps <= win else i % win)
+
+
+def stream_check(m, ptoks, n):
+    """teacher-forced stream check: seeded non-repeating tokens through per-step llama_eval and
+    through lvk_decode_chain; every step's device logits digest must equal the digest of the
+    per-step logits row"""
+    import lvk
+    from oracle_lib import forced_tokens
+    if n <= 0:
+        return None
+    seq_f = forced_tokens(n)
+    m.eval(ptoks, 0)
+    want = [lvk.logits_digest(m.eval([int(t)], len(ptoks) + i)[-1]) for i, t in enumerate(seq_f)]
+    m.eval(ptoks, 0)
+    _, got = m.decode_chain(seq_f, len(ptoks))
+    return {"steps": len(seq_f), "positions": "%d..%d" % (len(ptoks), len(ptoks) + len(seq_f) - 1),
+            "tokens": "oracle_lib.forced_tokens (seeded, non-repeating)",
+            "digests_equal": got.tolist() == want, "first_digests": [hex(d) for d in want[:3]]}
 
 
 if __name__ == "__main__":

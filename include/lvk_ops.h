@@ -96,6 +96,9 @@ LVK_API int lvk_get_profile(struct llama_context * ctx, double * ms, long * laun
 LVK_API void lvk_reset_profile(struct llama_context * ctx);
 /* bytes of quantized weights resident in HBM for this context's model */
 LVK_API size_t lvk_weight_bytes(struct llama_context * ctx);
+/* bytes of the prompt matmul's f16 A-fragment images (+ the Q4_1 side images) resident in
+ * HBM; 0 when they were not built (LVK_PROMPT_A16=0, or too little free memory at load) */
+LVK_API size_t lvk_prompt_image_bytes(struct llama_context * ctx);
 /* 1 = prompt batches (N > 1) use the bit-faithful VALU matmuls (the reference's
  * exact fp32 chain order), 0 = the MFMA matmuls (default; env LVK_PROMPT_EXACT=1
  * makes 1 the default) */

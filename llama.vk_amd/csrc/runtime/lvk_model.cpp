@@ -295,10 +295,12 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
         LVK_HIP(launch_repack(stage, q.qtype, q.M, q.K, (uint4 *) q.nib, (void *) q.scl, s, interleave4));
         if (a16 && q.qtype == Q4_0 && mm_mfma_supported(q)) {
             q.a16 = m.alloc(mm_a16_bytes(q.M, q.K));
+            m.prompt_image_bytes += mm_a16_bytes(q.M, q.K);
             LVK_HIP(launch_build_a16(q, (void *) q.a16, s));
         } else if (a16 && q.qtype == Q4_1 && q.M % 128 == 0 && q.K % 256 == 0) {
             q.a16 = m.alloc(mm_a16_bytes(q.M, q.K));
             q.side = m.alloc(mm41_side_bytes(q.M, q.K));
+            m.prompt_image_bytes += mm_a16_bytes(q.M, q.K) + mm41_side_bytes(q.M, q.K);
             LVK_HIP(launch_build_mm41(q, (void *) q.a16, (void *) q.side, s));
         }
         LVK_HIP(hipStreamSynchronize(s));

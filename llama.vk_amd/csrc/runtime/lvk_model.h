@@ -65,6 +65,7 @@ struct Model {
     bool has_head = true;          // last stage: final norm + lm_head resident
     std::vector<DevBuf> bufs;      // owned device memory
     size_t weight_bytes = 0;       // bytes of weights resident in HBM (quad-sliced images)
+    size_t prompt_image_bytes = 0; // the prompt matmul's f16 A-fragment (+ Q4_1 side) images
     size_t file_bytes = 0;
     std::string path;              // the model file (llama_internal_get_tensor_map re-maps it)
     double load_ms = 0;

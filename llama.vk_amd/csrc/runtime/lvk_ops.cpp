@@ -316,6 +316,11 @@ size_t lvk_weight_bytes(struct llama_context * ctx) {
     for (lvk::Context * c : ctx->stages()) b += c->model.weight_bytes;
     return b;
 }
+size_t lvk_prompt_image_bytes(struct llama_context * ctx) {
+    size_t b = 0;
+    for (lvk::Context * c : ctx->stages()) b += c->model.prompt_image_bytes;
+    return b;
+}
 void lvk_set_graph(struct llama_context * ctx, int on) {
     for (lvk::Context * c : ctx->stages()) c->use_graph = on != 0;
 }

@@ -107,6 +107,7 @@ _sig("lvk_set_profiling", None, [C.c_void_p, C.c_int])
 _sig("lvk_get_profile", C.c_int, [C.c_void_p, f64p, i64p, f64p, C.c_int])
 _sig("lvk_reset_profile", None, [C.c_void_p])
 _sig("lvk_weight_bytes", C.c_size_t, [C.c_void_p])
+_sig("lvk_prompt_image_bytes", C.c_size_t, [C.c_void_p])
 _sig("lvk_set_graph", None, [C.c_void_p, C.c_int])
 _sig("lvk_set_prompt_exact", None, [C.c_void_p, C.c_int])
 _sig("lvk_eval_greedy", C.c_int, [C.c_void_p, C.c_int, C.c_int])
@@ -351,6 +352,9 @@ class Llama:
 
     def weight_bytes(self):
         return int(lib.lvk_weight_bytes(self.ctx))
+
+    def prompt_image_bytes(self):
+        return int(lib.lvk_prompt_image_bytes(self.ctx))
 
     def print_timings(self):
         lib.llama_print_timings(self.ctx)
