@@ -229,8 +229,10 @@ LVK_API int lvk_stage_link_probe(struct llama_context * ctx, int bytes, int iter
  * bookkeeping, out[7] of them the microseconds in clear_refs.  Fills min(n, 8) values,
  * returns 8 (-1 on bad arguments).
  * lvk_ggml_invalidate: the caller changed [p, p + n) in a way that tracking cannot see
- * (write-enabled a read-only buffer, wrote, protected it again between two calls); its
- * pages are uploaded again by the next call.  0 / -1. */
+ * (write-enabled a read-only buffer, wrote, protected it again between two calls; or
+ * hipHostRegister'ed the range after a call had used it, so that DMA may now write it);
+ * its pages are uploaded again by the next call, and whether the range is HIP host memory
+ * is decided again.  0 / -1. */
 LVK_API int lvk_ggml_stats(uint64_t * out, int n);
 LVK_API int lvk_ggml_invalidate(const void * p, size_t n);
 

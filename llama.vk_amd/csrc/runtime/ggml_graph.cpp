@@ -720,6 +720,7 @@ struct Mirror {
     std::vector<int32_t> ro;       // per page: the read-only mapping it was uploaded from, or -1
     uint64_t last_call = 0;
     int hip_host = -1;             // 1: HIP-registered / pinned host memory (never cached); -1 unknown
+    uint64_t maps_sig = 0;         // the mappings over [lo, hi) when hip_host was decided
     uintptr_t page0() const { return (uintptr_t) lo / PAGE; }
     size_t pages() const { return (uintptr_t) (hi - 1) / PAGE - page0() + 1; }
 };
@@ -877,21 +878,42 @@ struct GraphEngine {
     void refresh_validity(Mirror & m) {
         DirtyTracker & T = tracker();
         if (!T.enabled) { std::fill(m.valid.begin(), m.valid.end(), 0); return; }
-        // host memory HIP can DMA into (registered or pinned): no CPU-side tracking sees those writes
-        if (m.hip_host < 0) {
-            hipPointerAttribute_t a{};
-            const bool lo_host = hipPointerGetAttributes(&a, m.lo) == hipSuccess && a.type == hipMemoryTypeHost;
-            (void) hipGetLastError();
-            hipPointerAttribute_t b{};
-            const bool hi_host = hipPointerGetAttributes(&b, m.hi - 1) == hipSuccess && b.type == hipMemoryTypeHost;
-            (void) hipGetLastError();
-            m.hip_host = lo_host || hi_host ? 1 : 0;
+        // host memory HIP can DMA into (registered or pinned): no CPU-side tracking sees those
+        // writes.  Decided per mirror from its first and last byte (a mirror that spans several
+        // allocations with a pinned one in the middle is not detected: probing the mappings in
+        // between can reach driver mappings), and decided again whenever the set of mappings
+        // over the range changed.  A range passed to hipHostRegister after its first use keeps
+        // its mappings: the caller says so with lvk_ggml_invalidate (lvk_ops.h), which also
+        // drops this decision.
+        {
+            uint64_t sig = 1469598103934665603ull;
+            for (const MapEnt & e : maps_now) {
+                if (e.hi <= (uintptr_t) m.lo || e.lo >= (uintptr_t) m.hi) continue;
+                for (uint64_t v : {(uint64_t) e.lo, (uint64_t) e.hi, e.inode, e.off}) sig = (sig ^ v) * 1099511628211ull;
+            }
+            if (sig != m.maps_sig) { m.hip_host = -1; m.maps_sig = sig; }
+            if (m.hip_host < 0) {
+                m.hip_host = 0;
+                for (const char * q : {(const char *) m.lo, (const char *) m.hi - 1}) {
+                    // only addresses mapped now: part of a mirror's range may have been unmapped
+                    // since it was mirrored (a freed scratch buffer), and HIP's pointer query
+                    // faults on some unmapped host addresses
+                    if (!map_of(maps_now, (uintptr_t) q)) continue;
+                    hipPointerAttribute_t a{};
+                    if (hipPointerGetAttributes(&a, q) == hipSuccess && a.type == hipMemoryTypeHost) m.hip_host = 1;
+                    (void) hipGetLastError();
+                }
+            }
         }
         if (m.hip_host == 1) { std::fill(m.valid.begin(), m.valid.end(), 0); return; }
         if (T.ok) {
-            // soft-dirty bits, read per run of pages; runs inside a read-only private mapping are
-            // skipped: without a write permission (a change of it shows in maps_now) the process
-            // cannot have written them, and a 7B / 65B weight mirror is almost all such pages
+            // soft-dirty bits, read per run of pages.  A page uploaded from a read-only private
+            // mapping that is still the same mapping (ro_alive: same range, offset, inode, device
+            // and permissions) is kept without a read -- the process cannot have written it, and
+            // a 7B / 65B weight mirror is almost all such pages.  A page whose mapping is gone or
+            // was replaced (munmap + mmap of another file at the same range) is dropped; a page
+            // uploaded while writable that now sits in a read-only mapping (written, then
+            // mprotect'ed) has its soft-dirty bit read like any writable page.
             std::vector<uint64_t> e;
             const size_t np = m.pages();
             auto it = maps_now.begin();
@@ -903,12 +925,20 @@ struct GraphEngine {
                 size_t j = i + 1;
                 while (j < np && (m.page0() + j) * PAGE < lim) ++j;
                 const bool ro = inside && !strchr(it->perms, 'w') && it->perms[3] == 'p';
-                if (!ro) {
+                bool need_read = !ro;
+                if (ro) {
+                    for (size_t k = i; k < j; ++k) {
+                        if (!m.valid[k]) continue;
+                        if (m.ro[k] < 0) need_read = true;                        // uploaded writable
+                        else if (!ro_alive[(size_t) m.ro[k]]) m.valid[k] = 0;     // another mapping
+                    }
+                }
+                if (need_read) {
                     if (!T.read(m.page0() + i, j - i, e)) {
                         std::fill(m.valid.begin() + i, m.valid.begin() + j, 0);
                     } else {
                         for (size_t k = 0; k < e.size(); ++k)
-                            if (DirtyTracker::written(e[k])) m.valid[i + k] = 0;
+                            if ((!ro || m.ro[i + k] < 0) && DirtyTracker::written(e[k])) m.valid[i + k] = 0;
                     }
                 }
                 i = j;
@@ -940,7 +970,9 @@ struct GraphEngine {
     void upload(Mirror & m, const char * a, const char * b) {
         const size_t np = m.pages();
         const size_t i0 = (uintptr_t) a / PAGE - m.page0(), i1 = std::min(np, (uintptr_t) (b - 1) / PAGE - m.page0() + 1);
-        const bool track_ro = tracker().enabled && !tracker().ok;
+        // the mapping identity of every page uploaded from a read-only mapping, in both caching
+        // modes (refresh_validity drops the page when that mapping is no longer the same one)
+        const bool track_ro = tracker().enabled;
         for (size_t i = i0; i < i1;) {
             if (m.valid[i]) { ++i; continue; }
             size_t j = i;
@@ -1262,9 +1294,11 @@ extern "C" void ggml_graph_compute(struct ggml_context * ctx, struct ggml_cgraph
             if (!regions.empty() && r.lo <= regions.back().hi) regions.back().hi = std::max(regions.back().hi, r.hi);
             else regions.push_back(r);
         }
-        // mirrors: created or merged
+        // mirrors: created or merged.  A later region's ensure() may merge (and delete) the mirror
+        // an earlier region got, so the mirrors this call uses are looked up after all merges
+        for (const Span & r : regions) R.ensure((char *) r.lo, (char *) r.hi);
         for (const Span & r : regions) {
-            Mirror & m = R.ensure((char *) r.lo, (char *) r.hi);
+            Mirror & m = R.mirror_of(r.lo);
             if (m.last_call != R.calls) {
                 m.last_call = R.calls;
                 R.used.push_back(&m);
@@ -1407,6 +1441,7 @@ extern "C" int lvk_ggml_invalidate(const void * p, size_t n) {
                 const size_t i0 = (uintptr_t) std::max(a, (const char *) m->lo) / PAGE - m->page0();
                 const size_t i1 = (uintptr_t) (std::min(b, (const char *) m->hi) - 1) / PAGE - m->page0() + 1;
                 for (size_t i = i0; i < i1; ++i) m->valid[i] = 0;
+                m->hip_host = -1;      // e.g. the range was hipHostRegister'ed since its first use
             }
             R.drop_repacked(a, b);
         }

@@ -71,12 +71,14 @@ def test_graph_compute_uploads_weights_once(gpu_available, wtype, cache, tmp_pat
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cache", ["1", "2"])
-@pytest.mark.parametrize("mode", ["private", "pinned", "shared"])
+@pytest.mark.parametrize("mode", ["private", "pinned", "shared", "remap", "mprotect"])
 def test_graph_compute_sees_untracked_host_writes(gpu_available, mode, cache):
     """the mirrors must not keep a stale device copy of host bytes that change where the CPU
     page tables cannot see it between two calls: a hipMemcpy D2H (DMA) into a pinned context
     buffer, a write through a second MAP_SHARED view of the buffer's pages, and a plain CPU
-    write (tools/ggml_graph/volatile_test.cpp: z = x + y checked after each); under the
+    write, a read-only file mapping replaced by another file's at the same address, and pages
+    written and then made read-only (tools/ggml_graph/volatile_test.cpp: z = x + y checked
+    after each); under the
     default caching (1) and under the opt-in soft-dirty tracking of writable pages (2)"""
     b = os.path.join(os.path.dirname(LVK_BIN), "volatile_test")
     if not os.path.exists(b):

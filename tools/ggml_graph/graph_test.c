@@ -18,7 +18,10 @@
  * against the reference ggml.c) -- the bytes each call moved are printed to stderr.
  */
 #define _GNU_SOURCE   /* mmap MAP_ANONYMOUS, clock_gettime under -std=c11 */
+#include <execinfo.h>
 #include <math.h>
+#include <signal.h>
+#include <unistd.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -66,7 +69,18 @@ struct layer {
     struct ggml_tensor *an, *fn, *wq, *wk, *wv, *wo, *w1, *w2, *w3;
 };
 
+/* a crash prints its raw backtrace (addresses map to the library with addr2line) */
+static void on_fault(int sig) {
+    void * bt[64];
+    const int n = backtrace(bt, 64);
+    backtrace_symbols_fd(bt, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 int main(int argc, char ** argv) {
+    signal(SIGSEGV, on_fault);
+    signal(SIGBUS, on_fault);
     if (argc < 4) {
         fprintf(stderr, "usage: %s out.bin wtype(0 q4_0, 1 q4_1) kv(1 f16, 0 f32)\n", argv[0]);
         return 2;

@@ -5,9 +5,15 @@
 //   shared  the buffer is one view of a memfd mapped twice (MAP_SHARED); between the calls the
 //           input is rewritten through the OTHER view (this view's page table never sees it)
 //   private the buffer is plain private memory rewritten by the CPU (the tracked case)
+//   remap   x's bytes are a read-only private mapping of a file (as llama.cpp maps weights);
+//           between the calls that mapping is replaced by one of ANOTHER file at the same
+//           address (munmap + mmap MAP_FIXED): same range and permissions, other inode
+//   mprotect x's bytes are private anonymous memory, written and then made read-only
+//           (mprotect PROT_READ) between the calls
 // Each case builds z = x + y, computes it, changes x, computes again and checks z both times.
-// usage: volatile_test pinned|shared|private   (prints "ok <case>" and exits 0)
+// usage: volatile_test pinned|shared|private|remap|mprotect   (prints "ok <case>" and exits 0)
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
 #include <sys/mman.h>
 #include <unistd.h>
 
@@ -34,6 +40,17 @@ static int check(const ggml_tensor * z, const std::vector<float> & x, const std:
     return 0;
 }
 
+// a temporary file holding the floats v (unlinked at once; the mapping keeps it alive)
+static int temp_file(const std::vector<float> & v) {
+    char name[] = "/tmp/lvk_volatile_XXXXXX";
+    const int fd = mkstemp(name);
+    if (fd < 0) { perror("mkstemp"); exit(2); }
+    unlink(name);
+    const size_t n = v.size() * 4;
+    if (write(fd, v.data(), n) != (ssize_t) n) { perror("write"); exit(2); }
+    return fd;
+}
+
 int main(int argc, char ** argv) {
     const char * mode = argc > 1 ? argv[1] : "private";
     const size_t mem = 8 << 20;
@@ -58,7 +75,19 @@ int main(int argc, char ** argv) {
     ggml_tensor * z = ggml_add(ctx, x, y);
     std::vector<float> xv(n), yv(n);
     for (int i = 0; i < n; ++i) { xv[i] = (float) i; yv[i] = 0.5f * (float) (i % 977); }
-    memcpy(x->data, xv.data(), n * 4);
+    const size_t xbytes = ((size_t) n * 4 + 4095) & ~(size_t) 4095;
+    if (!strcmp(mode, "remap")) {
+        void * p = mmap(nullptr, xbytes, PROT_READ, MAP_PRIVATE, temp_file(xv), 0);
+        if (p == MAP_FAILED) { perror("mmap"); return 2; }
+        x->data = p;
+    } else if (!strcmp(mode, "mprotect")) {
+        void * p = mmap(nullptr, xbytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) { perror("mmap"); return 2; }
+        x->data = p;
+        memcpy(x->data, xv.data(), n * 4);
+    } else {
+        memcpy(x->data, xv.data(), n * 4);
+    }
     memcpy(y->data, yv.data(), n * 4);
     ggml_cgraph g = ggml_build_forward(z);
     ggml_graph_compute(ctx, &g);
@@ -74,6 +103,15 @@ int main(int argc, char ** argv) {
         CK(hipFree(d));
     } else if (!strcmp(mode, "shared")) {
         memcpy(other + ((char *) x->data - buf), xv.data(), n * 4);
+    } else if (!strcmp(mode, "remap")) {
+        // another file at the same address, read-only and private like the first
+        const int fd = temp_file(xv);
+        if (munmap(x->data, xbytes) != 0) { perror("munmap"); return 2; }
+        void * p = mmap(x->data, xbytes, PROT_READ, MAP_PRIVATE | MAP_FIXED, fd, 0);
+        if (p != x->data) { perror("mmap fixed"); return 2; }
+    } else if (!strcmp(mode, "mprotect")) {
+        memcpy(x->data, xv.data(), n * 4);
+        if (mprotect(x->data, xbytes, PROT_READ) != 0) { perror("mprotect"); return 2; }
     } else {
         memcpy(x->data, xv.data(), n * 4);
     }
