@@ -155,7 +155,9 @@ int main(int argc, char ** argv) {
     unsigned * cnt; CK(hipMalloc(&cnt, NK * 1024)); CK(hipMemset(cnt, 0, NK * 1024));
     unsigned * err; CK(hipMalloc(&err, 64)); CK(hipMemset(err, 0, 64));
     unsigned long long * ts; CK(hipMalloc(&ts, NK * 16));
-    hipStream_t s[2]; CK(hipStreamCreate(&s[0])); CK(hipStreamCreate(&s[1]));
+    hipStream_t s[2];
+    if (getenv("OV_NONBLOCKING")) { CK(hipStreamCreateWithFlags(&s[0], hipStreamNonBlocking)); CK(hipStreamCreateWithFlags(&s[1], hipStreamNonBlocking)); }
+    else { CK(hipStreamCreate(&s[0])); CK(hipStreamCreate(&s[1])); }
     printf("mode %s, token bytes %.1f MB, %d launches, attention spin %.1f us\n", mode, total / 1e6, NK, spin_us);
 
     auto params = [&](int k, int tok, bool stamp) {
@@ -187,6 +189,8 @@ int main(int argc, char ** argv) {
     auto token = [&](bool stamp) {
         for (int k = 0; k < NK; ++k) {
             if (!strcmp(mode, "two")) launch(k, tok, stamp, s[k & 1], 0);
+            // "mixed": only the launch after each attention (Wo) is any-order, as in the library
+            else if (!strcmp(mode, "mixed")) launch(k, tok, stamp, s[0], (k % 5 == 2) ? hipExtAnyOrderLaunch : 0);
             else launch(k, tok, stamp, s[0], !strncmp(mode, "any", 3) ? hipExtAnyOrderLaunch : 0);
         }
         ++tok;
