@@ -99,10 +99,6 @@ __device__ unsigned long long g_dtrace[32 * 4 * 4 * 16];
 #define LVK_DT(ev) do { } while (0)
 #endif
 
-#ifdef LVK_PROBE_OVSTAMP   // dev probe build only (make ovstamp): per-workgroup entry / exit realtime stamps
-__device__ unsigned long long g_ovs_attn[128 * 1024 * 2];
-#endif
-
 struct AttnDArgs {
     const uint16_t * q16;
     const uint16_t * kc;
@@ -119,7 +115,6 @@ struct AttnDArgs {
     unsigned * err;               // host-mapped error word (nullptr: none)
     int short_max;                // n_kv <= short_max: no score exchange (every workgroup scores all)
     int seq_epochs;               // epoch += sp->seq << 7 (granules never zeroed between tokens)
-    OvWait ov;                    // overlapped step: wait for the QKV launch (CO), publish for Wo
 };
 
 // The 4 workgroups of a head either split the scores and exchange them as granules, or
@@ -127,9 +122,7 @@ struct AttnDArgs {
 // from the XCD's L2).  !DYN: always the exchange.  EM: the exp mode compiled in (exp_f16;
 // -1 reads A.exp_mode) -- a runtime mode puts the table path's load, and its vmcnt wait,
 // into the softmax loop.
-// CO: an overlapped step (lvk_kernels.h OvWait): the launch may start while the QKV launch still
-// runs, so it waits for the QKV workgroups' tags first and reads q, K and V by sc1 loads
-template <int QT, int EM, bool DYN = true, bool CO = false>
+template <int QT, int EM, bool DYN = true>
 __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, const int sl, uint8_t * smem,
                                            const int tid) {
     const int E = A.E, n_ctx = A.n_ctx, d0 = h * HD + sl * 32;
@@ -143,9 +136,6 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     auto bar = [&]() __attribute__((always_inline)) { lds_barrier(); };   // LDS hand-off barrier
     u64g * g = (u64g * ) (A.gran + (size_t) h * n_ctx);
     LVK_DT(0);
-#ifdef LVK_PROBE_OVSTAMP
-    if (tid == 0 && A.epoch <= 128) g_ovs_attn[((A.epoch - 1) * 1024 + h * 4 + sl) * 2] = __builtin_amdgcn_s_memrealtime();
-#endif
     // the step block through the scalar cache (constant address space: s_load, counted by
     // lgkmcnt): a vector load here would retire behind every Q / K / V load issued below
     // (vmcnt is in order) and hold the n_kv-dependent loads back by a full HBM latency
@@ -153,37 +143,17 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     const int n_past = spc->n_past;
     // this layer's granule tag: unique per (step, layer) when the step counter is used
     const unsigned ep = A.seq_epochs ? A.epoch + (spc->seq << 7) : A.epoch;
-    if constexpr (CO) {
-        // the QKV launch's tags (this layer's epoch too): wave 0 polls, the others wait at the
-        // barrier; every q / K / V load below is an sc1 load
-        if (tid < 64) {
-            for (int spins = 0;; ++spins) {
-                bool ok = true;
-                for (int q = 2 * tid; q < A.ov.n; q += 128) {
-                    const unsigned long long v = __hip_atomic_load((const unsigned long long *) (A.ov.ready + q),
-                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = ok && (unsigned) v == ep && (q + 1 >= A.ov.n || (unsigned) (v >> 32) == ep);
-                }
-                if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-                if (spins > LVK_SPIN_LIMIT) { if (tid == 0) raise_error(A.err, LVK_ERR_ATTN_SPIN); break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        asm volatile("s_barrier" ::: "memory");
-    }
-    // q / K rows: 16-byte loads at a byte offset from the cache base (sc1 when CO)
-    auto ldq = [&](const uint16_t * base, size_t elem) __attribute__((always_inline)) {
-        if constexpr (CO) return ld_co4(base, (uint32_t) (elem * 2));
-        else return *(const uint4 *) (base + elem);
-    };
 
     // 1a. Loads that do not depend on n_past go out before the step block is read: Q and
     // the K rows of positions 0..63 (chunk 0; rows past n_kv are read, never used).  A short
     // context (n_kv <= 64, no exchange) then has its score operands in flight from the
     // first cycle; V follows behind the first scores (1b).
     uint4 qv[4];
+    {
+        const uint4 * qp = (const uint4 *) (A.q16 + h * HD) + r;
 #pragma unroll
-    for (int st = 0; st < 4; ++st) qv[st] = ldq(A.q16, (size_t) h * HD + r * 8 + st * 32);
+        for (int st = 0; st < 4; ++st) qv[st] = qp[st * 4];
+    }
     auto v_dma = [&](int p0, int lo, int lim) {     // positions [max(p0, lo), min(p0 + 512, lim)) of rows 8 wave ..
 #pragma unroll
         for (int i = 0; i < 8; ++i) {               // a static count: the score waits can count past it
@@ -191,14 +161,15 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
             if (p0 + lane * 8 >= lo && p0 + lane * 8 < lim)
                 __builtin_amdgcn_global_load_lds((const void *) (A.vc + (size_t) (d0 + row) * n_ctx + p0 + lane * 8),
                                                  (__attribute__((address_space(3))) void *) (vl + (size_t) row * VS + p0),
-                                                 16, 0, CO ? 16 : 0);
+                                                 16, 0, 0);
         }
     };
     uint4 kv[2][4];
     {
         const int p = min(tid >> 2, n_ctx - 1);
+        const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
 #pragma unroll
-        for (int st = 0; st < 4; ++st) kv[0][st] = ldq(A.kc, (size_t) p * E + h * HD + r * 8 + st * 32);
+        for (int st = 0; st < 4; ++st) kv[0][st] = kp[st * 4];
     }
     const int n_kv = n_past + 1;
     const int n_pad = (n_kv + 31) & ~31;
@@ -211,13 +182,15 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     uint4 kx[4];
     if (c0_other) {
         const int p = min(sl * 64 + (tid >> 2), n_kv - 1);
+        const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
 #pragma unroll
-        for (int st = 0; st < 4; ++st) kx[st] = ldq(A.kc, (size_t) p * E + h * HD + r * 8 + st * 32);
+        for (int st = 0; st < 4; ++st) kx[st] = kp[st * 4];
     }
     {
         const int p = min((exch ? sl * 64 + 256 : 64) + (tid >> 2), n_kv - 1);
+        const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
 #pragma unroll
-        for (int st = 0; st < 4; ++st) kv[1][st] = ldq(A.kc, (size_t) p * E + h * HD + r * 8 + st * 32);
+        for (int st = 0; st < 4; ++st) kv[1][st] = kp[st * 4];
     }
     LVK_DT(6);
 
@@ -260,9 +233,10 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
         LVK_DT(1);
         for (int c0 = cb + 2 * cs; c0 < n_kv; c0 += cs) {
             const int p = c0 + (tid >> 2);
+            const uint4 * kp = (const uint4 *) (A.kc + (size_t) min(p, n_kv - 1) * E + h * HD) + r;
             uint4 k4[4];
 #pragma unroll
-            for (int st = 0; st < 4; ++st) k4[st] = ldq(A.kc, (size_t) min(p, n_kv - 1) * E + h * HD + r * 8 + st * 32);
+            for (int st = 0; st < 4; ++st) k4[st] = kp[st * 4];
             score(k4, p);
         }
     }
@@ -453,22 +427,8 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
             part |= __shfl_xor(part, 4);
             const uint32_t w0 = __shfl(part, 0), w1 = __shfl(part, 8), w2 = __shfl(part, 16), w3 = __shfl(part, 24);
             if (tid == 0) {
-                if (A.ov.pub) {
-                    // the overlapped Wo reads this block before any kernel boundary: write-through
-                    __hip_atomic_store(A.out.d + blk, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    uint32_t * qw = (uint32_t *) (A.out.qs + blk);
-                    __hip_atomic_store(qw + 0, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(qw + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(qw + 2, w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(qw + 3, w3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    // the stores have left the wave before the tag does (inline asm: the compiler's
-                    // wait-count pass may drop its own wait here, MI355X_MICROARCH.md compiler hazard)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_store(A.ov.pub + (h * 4 + sl), ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    A.out.d[blk] = dd;
-                    A.out.qs[blk] = make_uint4(w0, w1, w2, w3);
-                }
+                A.out.d[blk] = dd;
+                A.out.qs[blk] = make_uint4(w0, w1, w2, w3);
             }
         }
     }
@@ -487,9 +447,6 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
         }
     }
     LVK_DT(11);
-#ifdef LVK_PROBE_OVSTAMP
-    if (tid == 0 && A.epoch <= 128) g_ovs_attn[((A.epoch - 1) * 1024 + h * 4 + sl) * 2 + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
 }
 
 // LDS of one decode-attention workgroup (V slice, scores, probabilities, reductions)
@@ -521,24 +478,17 @@ inline AttnDArgs attn_args(const AttnLaunch & A, void * gran, unsigned epoch) {
     }();
     a.short_max = short_max;
     a.seq_epochs = A.seq_epochs;
-    a.ov = A.ov;
-    if (A.out_qtype != Q4_0 || A.out_f32) a.ov.pub = nullptr;    // only the Q4_0 Wo input is handed off
     return a;
 }
 
-template <int QT, int EM, bool CO = false>
+template <int QT, int EM>
 __global__ __launch_bounds__(256) void k_attn_d(AttnDArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    attn_d_run<QT, EM, true, CO>(A, blockIdx.x, blockIdx.y, smem, threadIdx.x);
+    attn_d_run<QT, EM, true>(A, blockIdx.x, blockIdx.y, smem, threadIdx.x);
 }
 
 }  // namespace
 
-#ifdef LVK_PROBE_OVSTAMP
-extern "C" __attribute__((visibility("default"))) void * lvk_probe_ovs_attn() {
-    void * p = nullptr; (void) hipGetSymbolAddress(&p, HIP_SYMBOL(g_ovs_attn)); return p;
-}
-#endif
 #ifdef LVK_PROBE_TIMING
 void * lvk_probe_dtrace() { void * p = nullptr; (void) hipGetSymbolAddress(&p, HIP_SYMBOL(g_dtrace)); return p; }
 #endif
@@ -548,8 +498,8 @@ bool attention_decode_supported(int n_embd, int n_head, int n_ctx) {
 }
 
 size_t attention_decode_scratch_bytes(int n_head, int n_ctx) {
-    // score granules [H][n_ctx], then the OvWait ready slots [H][4]
-    return (size_t) n_head * n_ctx * 8 + (size_t) n_head * 4 * 4;
+    // score granules [H][n_ctx]
+    return (size_t) n_head * n_ctx * 8;
 }
 
 hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned epoch, hipStream_t s) {
@@ -565,15 +515,7 @@ hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned e
         case 1: LVK_LAUNCH((k_attn_d<QT_, 1>), grid, dim3(256), lds, s, a); break;        \
         default: LVK_LAUNCH((k_attn_d<QT_, 0>), grid, dim3(256), lds, s, a); break;       \
     }
-    if (a.ov.ready) {
-        // an overlapped step (OvWait): any-order behind the QKV launch, Q4_0 Wo input only
-        if (A.out_qtype != Q4_0) return hipErrorNotSupported;
-        switch (a.exp_mode) {
-            case 2: LVK_LAUNCH_ANY((k_attn_d<Q4_0, 2, true>), grid, dim3(256), lds, s, a); break;
-            case 1: LVK_LAUNCH_ANY((k_attn_d<Q4_0, 1, true>), grid, dim3(256), lds, s, a); break;
-            default: LVK_LAUNCH_ANY((k_attn_d<Q4_0, 0, true>), grid, dim3(256), lds, s, a); break;
-        }
-    } else if (A.out_qtype == Q4_1) { LVK_ATTN_EM(Q4_1) } else { LVK_ATTN_EM(Q4_0) }
+    if (A.out_qtype == Q4_1) { LVK_ATTN_EM(Q4_1) } else { LVK_ATTN_EM(Q4_0) }
 #undef LVK_ATTN_EM
     return hipGetLastError();
 }

@@ -35,27 +35,6 @@ __device__ __forceinline__ void kv_store(uint16_t * base, size_t i, float v, int
     else base[i] = f32_to_f16(v);
 }
 
-// hand-offs between overlapped launches (lvk_kernels.h OvWait): write-through (sc1) stores and
-// sc1 loads (relaxed agent-scope atomics lower to plain global stores / loads with sc1)
-__device__ __forceinline__ float ld_co(const float * p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_co(float * p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_co(uint16_t * p, uint16_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_co(uint32_t * p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-// 16 bytes at base + byte_off by one sc1 buffer load (base wave-uniform, the offset per lane)
-__device__ __forceinline__ uint4 ld_co4(const void * base, uint32_t byte_off) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short) 0, 0x7fffffff, 0x00020000);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16);    // aux 16: sc1
-    return make_uint4(v[0], v[1], v[2], v[3]);
-}
-__device__ __forceinline__ float4 ld_co4f(const void * base, uint32_t byte_off) {
-    const uint4 u = ld_co4(base, byte_off);
-    return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
-}
-__device__ __forceinline__ void kv_store_co(uint16_t * base, size_t i, float v, int f32) {
-    if (f32) st_co((float *) base + i, v);
-    else st_co(base + i, f32_to_f16(v));
-}
-
 // table_exp_f16[h] (ggml.c:2915-2927: fp16(expf(fp16->f32(h))), built with the
 // host's glibc) for the arguments softmax produces (h <= 0, not NaN).
 // mode 0 reads the uploaded table; mode 1 computes exp in double, mode 2 with
@@ -142,11 +121,9 @@ __device__ __forceinline__ double warp_sum_d(double v) {
 // midpoint (r a normal float, or 0), else (about one row in 1e5) it returns the mean of an
 // index-order re-sum of x[0 .. n): the reference's float mean either way.
 // The cold path is out of line, so that its loop adds no registers to the kernels.
-// CO: x is handed over from a launch still running (OvWait): sc1 loads
-template <bool CO = false>
 __device__ __noinline__ float rms_mean_in_order(const float * x, int n) {
     double s = 0.0;
-    for (int i = 0; i < n; ++i) { const float v = CO ? ld_co(x + i) : x[i]; const float sq = v * v; s += (double) sq; }
+    for (int i = 0; i < n; ++i) { const float v = x[i]; const float sq = v * v; s += (double) sq; }
     return (float) (s / (double) n);
 }
 __device__ __forceinline__ float rms_mean(double tree, const float * x, int n) {
@@ -163,7 +140,6 @@ __device__ __forceinline__ float rms_mean(double tree, const float * x, int n) {
 // is a multiple of 2^m and the sum is below 2^(m+53), every partial sum in any order is exact,
 // so the tree's sum is the index-order one.  The synthetic models' activations carry few
 // significant bits and often sit exactly on a midpoint, and this certificate covers them.
-template <bool CO = false>
 __device__ __forceinline__ float rms_mean_wave(double tree, const float * x, int n) {
     const double r = tree / (double) n;
     const uint64_t rb = (uint64_t) __double_as_longlong(r);
@@ -173,7 +149,7 @@ __device__ __forceinline__ float rms_mean_wave(double tree, const float * x, int
     if (__builtin_expect(safe, 1)) return (float) r;
     int mlow = 1 << 20;            // lowest set-bit exponent over the nonzero squares
     for (int i = (int) (threadIdx.x & 63); i < n; i += 64) {
-        const float v = CO ? ld_co(x + i) : x[i];
+        const float v = x[i];
         const float sq = v * v;
         const uint32_t b = __float_as_uint(sq);
         if (b != 0u) {
@@ -184,7 +160,7 @@ __device__ __forceinline__ float rms_mean_wave(double tree, const float * x, int
     }
     for (int o = 32; o > 0; o >>= 1) { const int t = __shfl_xor(mlow, o); mlow = t < mlow ? t : mlow; }
     if (mlow == (1 << 20) || tree <= ldexp(1.0, mlow + 52)) return (float) r;
-    return rms_mean_in_order<CO>(x, n);
+    return rms_mean_in_order(x, n);
 }
 // whole-wave double sum through DPP (quad xor 1, xor 2, half-row and row
 // mirrors) and four readlanes; every lane returns the same value, and the

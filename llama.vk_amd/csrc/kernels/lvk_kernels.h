@@ -36,12 +36,6 @@ struct EventSplit {
         else                                                                                                   \
             hipLaunchKernelGGL(kern, grid, block, lds, stream, __VA_ARGS__);                                   \
     } while (0)
-// the same with the AQL barrier bit cleared (hipExtAnyOrderLaunch): the launch may start while
-// the previous one on the stream still runs -- only for kernels that wait for their inputs
-// themselves (OvWait below).  A captured graph keeps the barrier (the launch then just waits).
-#define LVK_LAUNCH_ANY(kern, grid, block, lds, stream, ...)                                                    \
-    hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ::lvk::g_launch_events.start,                        \
-                          ::lvk::g_launch_events.stop, hipExtAnyOrderLaunch, __VA_ARGS__)
 
 enum QType : int { Q4_0 = 2, Q4_1 = 3 };
 
@@ -101,27 +95,8 @@ enum Pro : int { PRO_NORM = 0, PRO_ACTQ = 1, PRO_ACTF = 2 /* f32 input, quantize
 // epilogue (what it does with row results)
 enum Epi : int { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_SWIGLU_F32 = 4, EPI_ROPE_KV = 5, EPI_SWIGLU_Q = 6 };
 
-// the hand-offs of an overlapped decode step (round 6).  Every launch of
-// the step after the first goes out any-order (LVK_LAUNCH_ANY), so it starts while its
-// predecessor still runs.  A producer launch stores every output a later launch of the step
-// reads write-through (sc1), waits for the stores, and then stores a tag into its slot of
-// `pub` (one per workgroup); a consumer issues its weight loads first, then polls until the n
-// slots of `ready` carry its tag, bounded (err gets LVK_ERR_ATTN_SPIN on a timeout), and reads
-// every handed-off byte with sc1 loads.  Tags: epoch + (seq << 7) when seq_epochs (epoch =
-// layer + 1, the decode attention's granule tags), so the slots are never zeroed per step.
-struct OvWait {
-    const unsigned * ready = nullptr;   // wait for the producer (nullptr: no wait)
-    int n = 0;
-    unsigned wait_epoch = 0;
-    unsigned * pub = nullptr;           // publish for the consumer (nullptr: ordinary stores)
-    unsigned pub_epoch = 0;
-    int seq_epochs = 0;
-    unsigned * err = nullptr;
-};
-
 struct MvLaunch {
     QMatrix w;
-    OvWait ov;                       // overlapped decode step (matvec_cu.hip PF 6)
     // input
     const float * x = nullptr;       // PRO_NORM: f32 [N][K]
     const float * g = nullptr;       // PRO_NORM: norm weight [K]
@@ -180,7 +155,6 @@ struct AttnLaunch {
     unsigned * err = nullptr; // host-mapped error word (DevError); kernels that spin report a timeout here
     int kv32 = 0;             // f32 K, V and queries (f16_kv = false): launch_attention only
     int seq_epochs = 0;       // decode attention: granule epoch = (sp->seq << 7) + epoch (no per-token zeroing)
-    OvWait ov;                // decode attention in an overlapped step: wait for the QKV launch, publish for Wo
 };
 hipError_t launch_attention(const AttnLaunch & A, hipStream_t s);
 // prompt batches (N > 1, Q4_0 / Q4_1 output): scores+softmax per (head, 32 tokens) then
@@ -201,10 +175,6 @@ hipError_t exp_check(const uint16_t * exp_tab, int * bad_d, hipStream_t s);
 // A.n_tokens == 1.
 bool attention_decode_supported(int n_embd, int n_head, int n_ctx);
 size_t attention_decode_scratch_bytes(int n_head, int n_ctx);
-// the decode attention's ready slots (OvWait::ready, 4 per head) inside that scratch
-inline unsigned * attention_decode_ready(void * gran, int n_head, int n_ctx) {
-    return (unsigned *) ((char *) gran + (size_t) n_head * n_ctx * 8);
-}
 hipError_t launch_attention_decode(const AttnLaunch & A, void * gran, unsigned epoch, hipStream_t s);
 
 // one-time weight repack: file-layout rows (ggml blocks) -> quad-sliced image

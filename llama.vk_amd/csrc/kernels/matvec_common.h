@@ -219,7 +219,7 @@ __device__ __forceinline__ uint32_t wsum_word(uint32_t w, bool other, uint32_t s
 // the q row / K-cache row / V-cache column stores (llama.cpp:996-1008).
 __device__ __forceinline__ void qkv_epilogue(float res, int row, int j, int E, int hd, int pos,
                                              const float2 * rope, uint16_t * q16, uint16_t * kc, uint16_t * vc,
-                                             int n_ctx, int kv32, bool co = false) {
+                                             int n_ctx, int kv32) {
     const int which = row / E;              // 0 q, 1 k, 2 v (uniform per wave: E % 8 == 0)
     const int e = row - which * E;
     const float other = __shfl_xor(res, 8);   // row e^1 lives in lanes of row r^1
@@ -231,16 +231,9 @@ __device__ __forceinline__ void qkv_epilogue(float res, int row, int j, int E, i
         else               { const float a = other * cs.y, b = res * cs.x; out = a + b; }
     }
     if (j == 0) {
-        // co: read by the overlapped decode attention before any kernel boundary (OvWait)
-        if (co) {
-            if (which == 0)      kv_store_co(q16, e, out, kv32);
-            else if (which == 1) kv_store_co(kc, (size_t) pos * E + e, out, kv32);
-            else                 kv_store_co(vc, (size_t) e * n_ctx + pos, out, kv32);
-        } else {
-            if (which == 0)      kv_store(q16, e, out, kv32);
-            else if (which == 1) kv_store(kc, (size_t) pos * E + e, out, kv32);
-            else                 kv_store(vc, (size_t) e * n_ctx + pos, out, kv32);
-        }
+        if (which == 0)      kv_store(q16, e, out, kv32);
+        else if (which == 1) kv_store(kc, (size_t) pos * E + e, out, kv32);
+        else                 kv_store(vc, (size_t) e * n_ctx + pos, out, kv32);
     }
 }
 

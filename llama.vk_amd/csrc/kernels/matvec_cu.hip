@@ -54,55 +54,7 @@ struct CuParams {
     int n_embd, head_dim, n_ctx;
     int kv32;                   // f32 KV cache and queries (f16_kv = false)
     const uint16_t * silu_tab;
-    OvWait ov;                  // overlapped decode step: wait (PF 6) and / or publish
 };
-
-#ifndef LVK_SPIN_LIMIT
-#define LVK_SPIN_LIMIT (1 << 22)
-#endif
-#ifdef LVK_PROBE_OVSTAMP   // dev probe build only (make ovstamp): PF 6 entry / wait-done / exit stamps
-__device__ unsigned long long g_ovs_wo[128 * 1024 * 3];
-#define LVK_OVS(ev) do { if (threadIdx.x == 0 && EPI == EPI_RESID && PRO == PRO_ACTQ && P.ov.wait_epoch && P.ov.wait_epoch <= 128) \
-    g_ovs_wo[((P.ov.wait_epoch - 1) * 1024 + blockIdx.x) * 3 + (ev)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define LVK_OVS(ev) do { } while (0)
-#endif
-
-// PF 6 (overlapped launch): wave 0 polls the producer's ready slots (8-byte relaxed agent
-// loads, sc1: two slots per lane and load) until every one carries this step's tag, bounded;
-// then a workgroup barrier, behind which every load of the handed-off bytes is an sc1 load
-// (MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire)
-__device__ __forceinline__ unsigned ov_tag(const CuParams & P, unsigned epoch) {
-    const __attribute__((address_space(4))) StepParams * spc = (const __attribute__((address_space(4))) StepParams *) P.sp;
-    return P.ov.seq_epochs ? epoch + (spc->seq << 7) : epoch;
-}
-__device__ __forceinline__ void ov_wait(const CuParams & P, int wave, int lane) {
-    if (wave == 0) {
-        const unsigned tag = ov_tag(P, P.ov.wait_epoch);
-        for (int spins = 0;; ++spins) {
-            bool ok = true;
-            for (int q = 2 * lane; q < P.ov.n; q += 128) {
-                const unsigned long long v = __hip_atomic_load((const unsigned long long *) (P.ov.ready + q),
-                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = ok && (unsigned) v == tag && (q + 1 >= P.ov.n || (unsigned) (v >> 32) == tag);
-            }
-            if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-            if (spins > LVK_SPIN_LIMIT) {
-                if (lane == 0 && P.ov.err)
-                    __hip_atomic_store(P.ov.err, (unsigned) LVK_ERR_ATTN_SPIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    asm volatile("s_barrier" ::: "memory");
-}
-// publish: every wave's output stores (sc1) have left it, then one tag per workgroup
-__device__ __forceinline__ void ov_publish(const CuParams & P) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) st_co(P.ov.pub + blockIdx.x, ov_tag(P, P.ov.pub_epoch));
-}
 
 // per-wave block-scale table s = dw * dx in LDS (two buffers, 8 rows x 32 blocks): the row
 // stride is padded to 40 floats so the rows start on banks 0, 40, 16, 56, 32, 8, 48, 24 of
@@ -131,14 +83,11 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
     [[maybe_unused]] int tq = 4;   // trace event index (probe builds)
     LVK_T(0);
 
-    constexpr bool OV = PF == 6;               // overlapped launch: weights, wait, then the inputs
     if (NP > 0 && wave >= NW) {
         // ---- prologue waves: build the activation table while the compute
         // waves put the CU's weight stream in flight (they never wait on x)
         const int pt = tid - NW * 64;
         constexpr int PT_ = PT > 0 ? PT : 64;   // (NP == 0: branch never taken)
-        // PF 6: the compute waves' wait (ov_wait's barrier) comes before the inputs
-        if constexpr (OV) asm volatile("s_barrier" ::: "memory");
         if constexpr (PRO == PRO_NORM || PRO == PRO_ACTF) {
             constexpr int UMP = (nunits + PT_ - 1) / PT_;
             float4 xv[UMP][2];
@@ -146,12 +95,8 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
 #pragma unroll
             for (int k = 0; k < UMP; ++k) {
                 const int un = min(k * PT_ + pt, nunits - 1);
-                if constexpr (OV) {
-                    xv[k][0] = ld_co4f(P.x, (uint32_t) un * 32); xv[k][1] = ld_co4f(P.x, (uint32_t) un * 32 + 16);
-                } else {
-                    const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
-                    xv[k][0] = xp[0]; xv[k][1] = xp[1];
-                }
+                const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
+                xv[k][0] = xp[0]; xv[k][1] = xp[1];
                 if constexpr (PRO == PRO_NORM) {
                     const float4 * gp = (const float4 *) (P.g + (size_t) un * 8);
                     gv[k][0] = gp[0]; gv[k][1] = gp[1];
@@ -161,11 +106,10 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
             float4 xs[XPL];
             if constexpr (PRO == PRO_NORM) {
 #pragma unroll
-                for (int i = 0; i < XPL; ++i)
-                    xs[i] = OV ? ld_co4f(P.x, (uint32_t) (i * 64 + lane) * 16) : ((const float4 *) P.x)[i * 64 + lane];
+                for (int i = 0; i < XPL; ++i) xs[i] = ((const float4 *) P.x)[i * 64 + lane];
             }
             // barrier A: the inputs enter the CU's texture queue ahead of the weight burst
-            if constexpr (!OV) __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_s_barrier();
             float scale = 1.0f;
             if constexpr (PRO == PRO_NORM) {
                 // ggml_compute_forward_rms_norm_f32 (ggml.c:6058-6076): every
@@ -182,7 +126,7 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
                 }
                 LVK_T(56);
                 acc = warp_sum_d(acc);
-                const float mean = rms_mean_wave<OV>(acc, P.x, KT);
+                const float mean = rms_mean_wave(acc, P.x, KT);
                 scale = 1.0f / sqrtf(mean + 1e-6f);
                 LVK_T(57);
             }
@@ -215,14 +159,14 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
                 if (un < nunits) act_store(act, dxp, un >> 2, un & 3, w, d, (un & 3) == 0);
             }
         } else {
-            if constexpr (!OV) __builtin_amdgcn_s_barrier();       // barrier A (see above)
+            __builtin_amdgcn_s_barrier();       // barrier A (see above)
             constexpr int UMP = (nb + PT_ - 1) / PT_;
 #pragma unroll
             for (int k = 0; k < UMP; ++k) {
                 const int b = k * PT_ + pt;
                 if (b < nb) {
-                    const uint4 qs = OV ? ld_co4(P.xq.qs, (uint32_t) b * 16) : P.xq.qs[b];
-                    const float d = OV ? ld_co(P.xq.d + b) : P.xq.d[b];
+                    const uint4 qs = P.xq.qs[b];
+                    const float d = P.xq.d[b];
                     act_store(act, dxp, b, 0, qs.x, d, true);
                     act_store(act, dxp, b, 1, qs.y, 0.0f, false);
                     act_store(act, dxp, b, 2, qs.z, 0.0f, false);
@@ -241,11 +185,7 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
     const int g0 = (int) ((unsigned) bid * (unsigned) P.G / (unsigned) nwg);     // G * n_cu < 2^32
     const int g1 = (int) ((unsigned) (bid + 1) * (unsigned) P.G / (unsigned) nwg);
     const int ng = max(0, (g1 - g0 - wave + NW - 1) / NW);      // row groups of this wave
-    if (NP > 0 && ng == 0) {
-        if constexpr (OV) ov_wait(P, wave, lane); else __builtin_amdgcn_s_barrier();
-        __syncthreads();
-        return;
-    }
+    if (NP > 0 && ng == 0) { __builtin_amdgcn_s_barrier(); __syncthreads(); return; }
     int gc = min(g0 + wave, P.G - 1);
 
     // NP == 0: the compute waves build the activation table themselves; its
@@ -257,7 +197,7 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
     float4 gv[UM][2];
     uint4 qv[UM];
     float dv[UM];
-    if constexpr (NP == 0 && !OV) {
+    if constexpr (NP == 0) {
         if constexpr (FPRO) {
 #pragma unroll
             for (int k = 0; k < UM; ++k) {
@@ -327,36 +267,9 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
     // weights keeps every wave of the CU in its issue for 1.3-4k cycles, so with 0 or 1 the
     // table (and the first chain) waits for the wave's own share of the burst to be issued.
     constexpr bool SPLIT = PF == 4 || PF == 5;
-    if constexpr (OV) LVK_OVS(0);
-    if constexpr (OV) {
-        // 6: the first D weight chunks in flight first (they do not depend on the producer),
-        // then the wait (its barrier also releases the prologue waves, NP > 0), then the
-        // producer's bytes by sc1 loads
-#pragma unroll
-        for (int d = 0; d < D; ++d) LVK_ISSUE(d, gc, d);
-        ov_wait(P, wave, lane);
-        LVK_OVS(1);
-        if constexpr (NP == 0) {
-#pragma unroll
-            for (int k = 0; k < UM; ++k) {
-                if constexpr (FPRO) {
-                    const int un = min(k * NT + tid, nunits - 1);
-                    xv[k][0] = ld_co4f(P.x, (uint32_t) un * 32); xv[k][1] = ld_co4f(P.x, (uint32_t) un * 32 + 16);
-                    if constexpr (PRO == PRO_NORM) {
-                        const float4 * gp = (const float4 *) (P.g + (size_t) un * 8);
-                        gv[k][0] = gp[0]; gv[k][1] = gp[1];
-                    }
-                } else {
-                    const int b = min(k * NT + tid, nb - 1);
-                    qv[k] = ld_co4(P.xq.qs, (uint32_t) b * 16);
-                    dv[k] = ld_co(P.xq.d + b);
-                }
-            }
-        }
-    }
-    if constexpr (PF != 0 && PF != 4 && !OV) launder_inputs();
+    if constexpr (PF != 0 && PF != 4) launder_inputs();
     // prologue waves (NP > 0): the weight burst goes out behind their inputs (barrier A)
-    if constexpr (NP > 0 && !OV) __builtin_amdgcn_s_barrier();
+    if constexpr (NP > 0) __builtin_amdgcn_s_barrier();
     LVK_T(58);
     if constexpr (PF <= 1) {
 #pragma unroll
@@ -391,7 +304,7 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
                 LVK_T(60);
                 double sum = red[0];
                 for (int w = 1; w < NW; ++w) sum += red[w];
-                const float mean = rms_mean_wave<OV>(sum, P.x, KT);
+                const float mean = rms_mean_wave(sum, P.x, KT);
                 scale = 1.0f / sqrtf(mean + 1e-6f);
             }
 #pragma unroll
@@ -541,29 +454,22 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
         return octet_reduce(acc);
     };
 
-    // overlapped step: the outputs are stored write-through and the residual read by an sc1
-    // load (a launch of this step still running may have written it)
-    const bool co = P.ov.pub != nullptr || P.ov.ready != nullptr;
     auto epilogue = [&](int grp, float res) __attribute__((always_inline)) {
         const int row = grp * 8 + r;
         if constexpr (EPI == EPI_STORE) {
             if (j == 0) P.y[row] = res;
         } else if constexpr (EPI == EPI_RESID) {
-            if (j == 0) {
-                if (co) st_co(P.y + row, res + ld_co(P.y + row));
-                else P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
-            }
+            if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
         } else if constexpr (EPI == EPI_QKV) {
             const StepParams * sp = P.sp;
-            qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32, co);
+            qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32);
         } else if constexpr (EPI == EPI_SWIGLU_F32) {
             // fused W1|W3 image interleaved per 4 rows: rows 0-3 of the group are
             // w1 rows 4grp..4grp+3, rows 4-7 the w3 rows (llama.cpp:1085-1096)
             const float a3 = __shfl_xor(res, 32);
             if (r < 4 && j == 0) {
                 const float sl = f16_to_f32(P.silu_tab[f32_to_f16(res)]);   // ggml_vec_silu_f32 (ggml.c:2495)
-                if (co) st_co(P.u + grp * 4 + r, sl * a3);
-                else P.u[grp * 4 + r] = sl * a3;                             // ggml_mul (llama.cpp:1096)
+                P.u[grp * 4 + r] = sl * a3;                                  // ggml_mul (llama.cpp:1096)
             }
         }
     };
@@ -580,8 +486,6 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
     const float res = body(std::false_type{}, gc, gc);
     epilogue(gc, res);
     LVK_T(3);
-    if constexpr (PF == 6) LVK_OVS(2);
-    if (P.ov.pub) ov_publish(P);
 #undef LVK_ISSUE
 }
 
@@ -605,18 +509,6 @@ static int mv_pf_env() {
 
 template <int NW, int NP, int D, int PRO, int EPI, int KT, int PFD = 2>
 hipError_t go(const CuParams & P, hipStream_t s) {
-    if constexpr (PFD == 6) {
-        constexpr int nb = KT / 32, NC = (nb + 31) / 32;
-        constexpr bool XG = (NC % D) == 0;
-        const int nwg = std::min(cu_count(), P.G);
-        if (!XG && (P.G + nwg - 1) / nwg > NW) return hipErrorNotSupported;
-        const size_t lds = (size_t) nb * 32 + NC * 128 + NW * 2 * SPL * 4 + NW * 8;
-        // LVK_OVERLAP=2 (A/B only): the same kernel behind an ordinary launch (barrier bit set)
-        static const bool any = [] { const char * e = getenv("LVK_OVERLAP"); return !e || atoi(e) != 2; }();
-        if (any) LVK_LAUNCH_ANY((k_mv_cu<NW, NP, D, PRO, EPI, KT, 6>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
-        else LVK_LAUNCH((k_mv_cu<NW, NP, D, PRO, EPI, KT, 6>), dim3(nwg), dim3((NW + NP) * 64), lds, s, P);
-        return hipGetLastError();
-    }
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
     constexpr bool XG = (NC % D) == 0;
     const int nwg = std::min(cu_count(), P.G);
@@ -656,11 +548,6 @@ int cu_count() {
     return n[dev];
 }
 
-#ifdef LVK_PROBE_OVSTAMP
-extern "C" __attribute__((visibility("default"))) void * lvk_probe_ovs_wo() {
-    void * p = nullptr; (void) hipGetSymbolAddress(&p, HIP_SYMBOL(g_ovs_wo)); return p;
-}
-#endif
 #ifdef LVK_PROBE_TIMING
 void * lvk_probe_trace() { void * p = nullptr; (void) hipGetSymbolAddress(&p, HIP_SYMBOL(g_trace)); return p; }
 #endif
@@ -687,7 +574,6 @@ CuParams cu_params(const MvLaunch & L) {
     P.q16 = L.q16; P.kc = L.kc; P.vc = L.vc; P.rope = L.rope.cs;
     P.n_embd = L.n_embd; P.head_dim = L.head_dim; P.n_ctx = L.n_ctx; P.kv32 = L.kv32;
     P.silu_tab = L.silu_tab;
-    P.ov = L.ov;
     return P;
 }
 }  // namespace
@@ -715,16 +601,6 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
     // launch shapes (waves NW, prefetch depth D) per row length and role, measured on
     // the 7B shapes (tools/probe, LVK_PROBE_SWEEP) and scaled for 65B: enough waves that
     // every CU keeps ~60-120 KB of weights in flight
-    if (P.ov.ready) {
-        // an overlapped decode step (lvk_kernels.h OvWait): the 7B shapes with prologue order 6
-        if (K == 4096 && epi == EPI_QKV && pro == PRO_NORM) return go<8, 0, 2, PRO_NORM, EPI_QKV, 4096, 6>(P, s);
-        if (K == 4096 && epi == EPI_SWIGLU_F32 && pro == PRO_NORM) return go<12, 0, 2, PRO_NORM, EPI_SWIGLU_F32, 4096, 6>(P, s);
-        if (K == 4096 && epi == EPI_STORE && pro == PRO_NORM) return go<16, 0, 2, PRO_NORM, EPI_STORE, 4096, 6>(P, s);
-        // Wo: the whole row group of each wave (4 chunks) goes out while the attention runs
-        if (K == 4096 && epi == EPI_RESID && pro == PRO_ACTQ) return go<2, 0, 4, PRO_ACTQ, EPI_RESID, 4096, 6>(P, s);
-        if (K == 11008 && epi == EPI_RESID && pro == PRO_ACTF) return go<2, 6, 4, PRO_ACTF, EPI_RESID, 11008, 6>(P, s);
-        return hipErrorNotSupported;
-    }
     if (K == 4096) {
         switch (epi) {
             // prologue order 5 (inputs, chunk 0, table, the rest after the barrier): QKV 7.6 vs

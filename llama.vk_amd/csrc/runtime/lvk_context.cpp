@@ -129,15 +129,8 @@ void Context::init(const llama_context_params & p) {
         uf = (float *) model.alloc(C * F * 4);
         prompt_exact = getenv("LVK_PROMPT_EXACT") && atoi(getenv("LVK_PROMPT_EXACT")) != 0;
         old_attention = getenv("LVK_ATTN_V1") && atoi(getenv("LVK_ATTN_V1")) != 0;
-        {
-            const char * e = getenv("LVK_OVERLAP");
-            overlap = e && atoi(e) != 0;
-        }
         attn_gran = model.alloc(attention_decode_scratch_bytes((int) H, (int) C));
         LVK_HIP(hipMemset(attn_gran, 0, attention_decode_scratch_bytes((int) H, (int) C)));
-        // the overlapped decode step's ready slots (QKV, Wo, W1|W3, W2; 1024 workgroups each)
-        ov_slots = (unsigned *) model.alloc(4 * 1024 * 4);
-        LVK_HIP(hipMemset(ov_slots, 0, 4 * 1024 * 4));
         // granule tags (seq << 7) + layer + 1 stay unique per token with up to 126 layers
         seq_epochs = L <= 126;
         // test hook (tests/test_gpu_seq_wrap.py): start the step counter near its 25-bit wrap
@@ -242,8 +235,7 @@ static double qbytes(const QMatrix & w) { return (double) w.M * (w.K / 32) * (w.
 static hipError_t mv_launch(const MvLaunch & L, int pro, int epi, hipStream_t s) {
     if (L.n_tokens == 1 && matvec_cu_supported(L.w.K, L.w.qtype)) {
         const hipError_t e = launch_matvec_cu(L, pro, epi, s);
-        // an overlapped launch has no other kernel (the generic ones neither wait nor publish)
-        if (e != hipErrorNotSupported || L.ov.ready || L.ov.pub) return e;
+        if (e != hipErrorNotSupported) return e;
     }
     return launch_matvec(L, pro, epi, s);
 }
@@ -350,18 +342,6 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
     // single-token FFN: W1|W3 hands silu(w1 x)*(w3 x) to W2 in f32, W2 quantizes it
     const bool ffn_f32 = n == 1 && matvec_cu_supported(E, model.qtype) && matvec_cu_supported(F, model.qtype);
     const bool seq_ep = seq_epochs;
-    // the overlapped decode step (lvk_kernels.h OvWait): every launch after
-    // the first QKV goes out any-order and waits for its producer's tags.  Eager enqueue only (a
-    // captured graph keeps the barrier bits), the whole 7B-shaped Q4_0 model on one device with
-    // one workgroup per CU for every decode matvec
-    const bool ov = overlap && !in_capture && !profiling && n == 1 && last_only && !old_attention && !kv32 &&
-                    model.qtype == Q4_0 && model.has_embed && model.has_head && head && embed && ov_slots &&
-                    E == 4096 && F == 11008 && H * 4 <= 1024 && cu_count() >= 256 &&
-                    attention_decode_supported(E, H, n_ctx);
-    // producer grids (one slot per workgroup): the decode matvecs run min(CUs, row groups)
-    auto grid_of = [&](int M) { return std::min(cu_count(), M / 8); };
-    unsigned * const s_qkv = ov_slots, * const s_wo = ov_slots + 1024, * const s_w13 = ov_slots + 2048,
-             * const s_w2 = ov_slots + 3072;
     if (n == 1 && !old_attention && attention_decode_supported(E, H, n_ctx) && !seq_ep)
         // the decode attention's score granules carry epoch = layer + 1: zero them once per token
         LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes(H, n_ctx), stream));
@@ -381,15 +361,6 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
         at.err = err_d;
         at.kv32 = kv32;
         at.seq_epochs = seq_ep ? 1 : 0;
-        const unsigned ep = (unsigned) il + 1;
-        const int sq = seq_ep ? 1 : 0;
-        unsigned * const s_att = attention_decode_ready(attn_gran, H, n_ctx);
-        if (ov) {
-            // QKV waits for the previous layer's W2 (layer 0: an ordinary launch after the embedding)
-            if (il > 0) a.ov = OvWait{s_w2, grid_of(E), (unsigned) il, nullptr, 0, sq, err_d};
-            a.ov.pub = s_qkv; a.ov.pub_epoch = ep; a.ov.seq_epochs = sq; a.ov.err = err_d;
-            at.ov = OvWait{s_qkv, grid_of(3 * E), ep, s_att, ep, sq, err_d};
-        }
         timed_launch(K_QKV, qbytes(ly.wqkv), [&] { return mv_launch(a, PRO_NORM, EPI_QKV, stream); });
         if (n > 1 && !kv32 && attention_prompt_supported(E, H, n_ctx))
             timed_launch(K_ATTN, 0, [&] { return launch_attention_prompt(at, (uint16_t *) scores, nullptr, nullptr, stream); });
@@ -399,17 +370,12 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
             timed_launch(K_ATTN, 0, [&] { return launch_attention(at, stream); });
         MvLaunch b;
         b.w = ly.wo; b.xq = aq_attn; b.y = x; b.sp = sp_d; b.n_tokens = n;
-        if (ov) b.ov = OvWait{s_att, H * 4, ep, s_wo, ep, sq, err_d};
         timed_launch(K_WO, qbytes(ly.wo), [&] { return mv_launch(b, PRO_ACTQ, EPI_RESID, stream); });
         MvLaunch c;
         c.w = ly.w13; c.x = x; c.g = ly.ffn_norm; c.sp = sp_d; c.n_tokens = n; c.silu_tab = silu_tab;
         c.out_q = aq_ffn; c.u = u_ffn;
         MvLaunch d;
         d.w = ly.w2; d.xq = aq_ffn; d.x = u_ffn; d.y = x; d.sp = sp_d; d.n_tokens = n;
-        if (ov) {
-            c.ov = OvWait{s_wo, grid_of(E), ep, s_w13, ep, sq, err_d};
-            d.ov = OvWait{s_w13, grid_of(2 * F), ep, s_w2, ep, sq, err_d};
-        }
         if (ffn_f32) {
             timed_launch(K_W13, qbytes(ly.w13), [&] { return launch_matvec_cu(c, PRO_NORM, EPI_SWIGLU_F32, stream); });
             timed_launch(K_W2, qbytes(ly.w2), [&] { return launch_matvec_cu(d, PRO_ACTF, EPI_RESID, stream); });
@@ -423,7 +389,6 @@ void Context::enqueue_forward(int n, bool last_only, const int * tok_src, int lo
     o.w = model.output; o.x = x; o.g = model.norm; o.sp = sp_d; o.y = logits_out;
     o.tok0 = last_only ? n - 1 : 0;
     o.n_tokens = last_only ? 1 : n;
-    if (ov) o.ov = OvWait{s_w2, grid_of(E), (unsigned) model.layers.size(), nullptr, 0, seq_ep ? 1 : 0, err_d};
     timed_launch(K_LMHEAD, qbytes(model.output), [&] { return mv_launch(o, PRO_NORM, EPI_STORE, stream); });
     if (want_embedding && model.has_head)
         LVK_HIP(launch_rmsnorm_rows(x + (size_t) (n - 1) * E, model.norm, E, 1, emb_d, stream));
@@ -439,17 +404,13 @@ void Context::build_graph(int kind) {
         if (kind == 3) {
             // a chained step: the step block and x were left by the previous step (or the
             // call's setup); the argmax advances both for the next replay
-            in_capture = true;
             enqueue_forward(1, true, nullptr, 0, true, false);
-            in_capture = false;
             LVK_HIP(launch_argmax_step(logits_d, (int) model.hp.n_vocab, sp_d, chain_d, forced_d, digest_d, model.tok_emb, model.emb_type,
                                        (int) model.hp.n_embd, x, stream));
         } else {
             LVK_HIP(hipMemcpyAsync(sp_d, sp_h, sizeof(StepParams), hipMemcpyHostToDevice, stream));
             if (kind == 2) LVK_HIP(hipMemcpyAsync(samp_d, samp_h, sizeof(SampleParams), hipMemcpyHostToDevice, stream));
-            in_capture = true;
             enqueue_forward(1, true);
-            in_capture = false;
             if (kind == 1) {
                 enqueue_argmax();
             } else if (kind == 2) {
@@ -460,7 +421,6 @@ void Context::build_graph(int kind) {
             }
         }
     } catch (...) {
-        in_capture = false;
         hipGraph_t g;
         (void) hipStreamEndCapture(stream, &g);
         throw;
@@ -497,7 +457,6 @@ unsigned Context::next_seq(unsigned k) {
     if (seq + k >= (1u << 25)) {
         if (attn_gran)
             LVK_HIP(hipMemsetAsync(attn_gran, 0, attention_decode_scratch_bytes((int) model.hp.n_head, n_ctx), stream));
-        if (ov_slots) LVK_HIP(hipMemsetAsync(ov_slots, 0, 4 * 1024 * 4, stream));
         seq = 0;
     }
     const unsigned first = seq + 1;
@@ -610,10 +569,7 @@ void Context::begin_eval(const int * tokens, int n, int n_past, const EvalPart &
     }
     const bool last_only = !logits_all;
     const bool single = part.n_total < 0 || part.n_total == n;
-    // the overlapped decode runs eagerly for plain evals (graph capture keeps every barrier bit);
-    // the greedy / sampling / chained graphs stay
-    const bool graph_ok = n == 1 && last_only && single && use_graph && !profiling &&
-                          !(overlap && !part.greedy && !part.sample);
+    const bool graph_ok = n == 1 && last_only && single && use_graph && !profiling;
     // the graphs read step block 0; eager slices each take their own (the H2D copy reads
     // the pinned block when it executes, after the host may have queued further slices)
     if (!graph_ok && sp_next > n_ctx) throw Error("llama.vk_amd: too many slices before a sync");

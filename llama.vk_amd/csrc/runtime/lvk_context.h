@@ -99,12 +99,6 @@ struct Context {
     // bit-faithful VALU kernels (prompt_exact; env LVK_PROMPT_EXACT=1)
     bool prompt_exact = false;
     bool old_attention = false;  // env LVK_ATTN_V1=1: single-token evals on the one-kernel attention.hip
-    // single-token llama_eval: Wo launched any-order behind the decode attention (its weight
-    // stream in flight while the attention runs, OvWait hand-off), the step enqueued eagerly
-    // (a captured graph keeps the barrier bit); env LVK_OVERLAP=0 turns it off
-    bool overlap = false;
-    bool in_capture = false;     // build_graph is capturing: ordinary launches only
-    unsigned * ov_slots = nullptr;   // [4][1024] OvWait tags of the QKV, Wo, W1|W3 and W2 launches
     void * attn_gran = nullptr;  // [H][n_ctx] {tag, score} granules of the decode attention
     uint16_t * xh = nullptr;     // masked MFMA B-fragment image of the quantized activations (mm_act_bytes)
     float * xda = nullptr;       // [Cpad][max(E,F)/32] their block scales
