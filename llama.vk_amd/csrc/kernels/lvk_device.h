@@ -242,18 +242,6 @@ __device__ __forceinline__ void mm_tile(int L, int ntt, int nrt, int supertile, 
     }
 }
 
-// fmaf(a, f16 half HB of b, c) with a and c in f32: v_fma_mix converts the f16 operand exactly
-// and rounds once, the same result as fmaf(a, (float) half, c)
-template <int HB>
-__device__ __forceinline__ float fma_mix_fh(float a, uint32_t b, float c) {
-    float d;
-    if constexpr (HB == 0)
-        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    else
-        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-}
-
 // fmaf(f16 half HA of a, f16 half HB of b, c): v_fma_mix converts both f16 operands
 // exactly and rounds once, the same result as fmaf on the converted values
 template <int HA, int HB>

@@ -217,6 +217,11 @@ inline bool prompt_a16_env() {
     const char * e = getenv("LVK_PROMPT_A16");
     return !e || atoi(e) != 0;
 }
+// LVK_PROMPT_A16=1: build the Q4_0 images whenever they fit; unset: by capacity (lvk_model.cpp)
+inline bool prompt_a16_forced() {
+    const char * e = getenv("LVK_PROMPT_A16");
+    return e && atoi(e) == 1;
+}
 hipError_t launch_mm_mfma(const QMatrix & w, const void * xm, const float * da, int N, float * y, int ldy,
                           int out_tok0, int epi, const uint16_t * silu_tab, hipStream_t s);
 // x[N][K] (rms_norm * g when g != nullptr) -> quantize_row_q4_0 -> xm, da

@@ -358,314 +358,6 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
 #undef LVK_ISSUE41
 }
 
-
-// ---------------------------------------------------------------------------------------------
-// Producer / consumer Q4_1 decode matvec (k_mv41_pc; round-6 verdict item 4) for the shapes
-// whose CU owns only 2-3 row groups (13B Wo, K 5120, and W2, K 13824: 640 groups on 256 CUs).
-// In k_mv_cu41 ONE wave per row group does all of a block's work -- the udot8 partials, the
-// weight / activation sums, the four product tables and the three chained updates -- and the
-// counters put these kernels at twice the Q4_0 VALU share (profiles/r05_sq_decode_13b.json).
-// The only serial part of ggml_vec_dot_q4_1 (ggml.c:2188-2258) is the chain itself:
-//   acc_j = fmaf(dx*dy, (float) p_j, acc_j); acc_j = fmaf(cross_j, (float) S_j, acc_j);
-//   off = off + mx*my                                          (block order, per row)
-// Here each row group has one CONSUMER wave that only runs those updates, and NPR PRODUCER
-// waves that stream the group's chunks (chunk pk, pk + NPR, ...) and turn each into the
-// consumer's operands in an LDS ring slot: per lane (row r, chain j) and block b one dword
-// {f16 p, f16 S} (integers below 1024 and 256: exact), and the four per-row product tables
-// dx*dy, dx*my, mx*dy, mx*my (k_mv_cu41's, same products).  The consumer reads them with
-// v_fma_mix (fmaf(f32, (float) f16, f32), one rounding) in block order and runs the epilogue:
-// bit-identical to k_mv_cu41 by construction.  Ring hand-offs are LDS words (tag = chunk + 1).
-constexpr int PC41_PS = 144;                              // bytes per lane of a slot's {p, S} area (32 dwords + pad)
-constexpr int PC41_SLOT = 64 * PC41_PS + SWF * 4;         // + the four product tables [4][8 rows][SRS]
-
-template <int GMAX, int NPR, int R, int PRO, int EPI, int KT>
-__global__ __launch_bounds__(GMAX * (1 + NPR) * 64) void k_mv41_pc(Cu41Params P) {
-    constexpr int NW = GMAX * (1 + NPR);
-    constexpr int NT = NW * 64;
-    constexpr int nb = KT / 32;
-    constexpr int nsub = nb / 8;
-    constexpr int NC = (nb + 31) / 32;
-    constexpr int nunits = KT / 8;
-    constexpr bool FPRO = (PRO == PRO_NORM || PRO == PRO_ACTF);
-    constexpr int CPP = (NC + NPR - 1) / NPR;          // chunks per producer (at most)
-    static_assert(nb % 8 == 0, "K must be a multiple of 256");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t * act = (uint32_t *) smem;                          // nb * 32 B
-    float * dyv = (float *) (smem + nb * 32);                    // NC * 32
-    float * myv = dyv + NC * 32;                                 // NC * 32
-    uint8_t * ys = (uint8_t *) (myv + NC * 32);                  // nb * 4 bytes: activation sums
-    uint8_t * ring = ys + ((nb * 4 + 15) & ~15);                 // GMAX * R slots
-    unsigned * full = (unsigned *) (ring + (size_t) GMAX * R * PC41_SLOT);   // [GMAX][R]
-    unsigned * freed = full + GMAX * R;                                       // [GMAX][R]
-    double * red = (double *) (freed + GMAX * R);                             // NW doubles
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int j = lane & 7, r = lane >> 3;
-    // consumers are waves 0..GMAX-1, then the producers of group 0, 1, ...
-    const bool consumer = wave < GMAX;
-    const int gi = consumer ? wave : (wave - GMAX) / NPR;
-    const int pk = consumer ? 0 : (wave - GMAX) - gi * NPR;
-    const int g0 = (int) ((unsigned) blockIdx.x * (unsigned) P.G / (unsigned) gridDim.x);
-    const int g1 = (int) ((unsigned) (blockIdx.x + 1) * (unsigned) P.G / (unsigned) gridDim.x);
-    const bool has = g0 + gi < g1;
-    const int grp = min(g0 + gi, P.G - 1);
-    uint8_t * gring = ring + (size_t) gi * R * PC41_SLOT;
-
-    // 1. the prologue inputs first (vmcnt retires in order)
-    constexpr int UM = FPRO ? (nunits + NT - 1) / NT : (nb + NT - 1) / NT;
-    float4 xv[UM][2];
-    float4 gv[PRO == PRO_NORM ? UM : 1][2];
-    uint4 qv[FPRO ? 1 : UM];
-    float dv[FPRO ? 1 : UM], mv_[FPRO ? 1 : UM];
-    if constexpr (FPRO) {
-#pragma unroll
-        for (int k = 0; k < UM; ++k) {
-            const int un = min(k * NT + tid, nunits - 1);
-            const float4 * xp = (const float4 *) (P.x + (size_t) un * 8);
-            xv[k][0] = xp[0]; xv[k][1] = xp[1];
-            if constexpr (PRO == PRO_NORM) {
-                const float4 * gp = (const float4 *) (P.g + (size_t) un * 8);
-                gv[k][0] = gp[0]; gv[k][1] = gp[1];
-            }
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < UM; ++k) {
-            const int b = min(k * NT + tid, nb - 1);
-            qv[k] = P.xq.qs[b];
-            dv[k] = P.xq.d[b];
-            mv_[k] = P.xq.m[b];
-        }
-    }
-    // producer weights: a two-chunk register ring; the first chunk goes out with the prologue
-    // inputs, the second after the table barrier.  Consumer (and idle) waves issue the same
-    // loads with every lane on one word: no branch separates the issue from the waits
-    const uint32_t loff = (has && !consumer) ? (uint32_t) lane * 16u : 0u;
-    const size_t gq = (size_t) grp * NC;
-    uint4 W[2][4], WS[2];
-    float4 SD[2], SM[2];
-    auto issue = [&](const int slot, const int i) __attribute__((always_inline)) {
-        const int cc = min(pk + i * NPR, NC - 1);
-#pragma unroll
-        for (int sb = 0; sb < 4; ++sb) {
-            // (a partial last chunk re-reads its last real sub-chunk; the slots are never used)
-            const int su = min(cc * 4 + sb, nsub - 1);
-            W[slot][sb] = ld_nt((const uint4 *) ((const char *) P.nib + gq * 4096 + (size_t) su * 1024 + loff));
-        }
-        const char * sc_ = (const char *) P.scl + (gq + cc) * 2048 + loff;
-        SD[slot] = *(const float4 *) sc_;
-        SM[slot] = *(const float4 *) (sc_ + 1024);
-        WS[slot] = ld_nt((const uint4 *) ((const char *) P.wsum + (gq + cc) * 1024 + loff));
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    issue(0, 0);
-#pragma unroll
-    for (int k = 0; k < UM; ++k) {
-        if constexpr (FPRO) {
-            launder(xv[k][0]); launder(xv[k][1]);
-            if constexpr (PRO == PRO_NORM) { launder(gv[k][0]); launder(gv[k][1]); }
-        } else {
-            launder(qv[k]); launder(dv[k]); launder(mv_[k]);
-        }
-    }
-    if (tid < 2 * GMAX * R) full[tid] = 0u;     // full and freed are adjacent
-
-    // 2. the activation table (every wave builds its share; k_mv_cu41's layout)
-    if constexpr (FPRO) {
-        float scale = 1.0f;
-        if constexpr (PRO == PRO_NORM) {
-            double acc = 0.0;
-#pragma unroll
-            for (int k = 0; k < UM; ++k) {
-                if (k * NT + tid < nunits) {
-                    const float e[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
-                                        xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) { const float sq = e[q] * e[q]; acc += (double) sq; }
-                }
-            }
-            acc = wave_sum_d(acc);
-            if (lane == 0) red[wave] = acc;
-            __syncthreads();
-            double sum = red[0];
-            for (int w = 1; w < NW; ++w) sum += red[w];
-            const float mean = rms_mean_wave(sum, P.x, KT);
-            scale = 1.0f / sqrtf(mean + 1e-6f);
-        }
-#pragma unroll
-        for (int k = 0; k < UM; ++k) {
-            if (k * NT >= nunits) break;
-            const int un = k * NT + tid;
-            float v[8] = {xv[k][0].x, xv[k][0].y, xv[k][0].z, xv[k][0].w,
-                          xv[k][1].x, xv[k][1].y, xv[k][1].z, xv[k][1].w};
-            if constexpr (PRO == PRO_NORM) {
-                const float gg[8] = {gv[k][0].x, gv[k][0].y, gv[k][0].z, gv[k][0].w,
-                                     gv[k][1].x, gv[k][1].y, gv[k][1].z, gv[k][1].w};
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float yn = v[e] * scale;      // ggml_vec_scale_f32 (ggml.c:6076)
-                    v[e] = gg[e] * yn;                  // ggml_mul(repeat(g), cur) (llama.cpp:984)
-                }
-            }
-            float d, m;
-            uint32_t qw;
-            q41_quad(v, d, m, qw);
-            uint32_t qs[4];
-            qs[0] = __builtin_bit_cast(uint32_t, quad_bcast<0>(__builtin_bit_cast(float, qw)));
-            qs[1] = __builtin_bit_cast(uint32_t, quad_bcast<1>(__builtin_bit_cast(float, qw)));
-            qs[2] = __builtin_bit_cast(uint32_t, quad_bcast<2>(__builtin_bit_cast(float, qw)));
-            qs[3] = __builtin_bit_cast(uint32_t, quad_bcast<3>(__builtin_bit_cast(float, qw)));
-            if (un < nunits && (un & 3) == 0) act41_store(act, dyv, myv, ys, un >> 2, qs, d, m);
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < UM; ++k) {
-            const int b = k * NT + tid;
-            if (b < nb) {
-                const uint32_t qs[4] = {qv[k].x, qv[k].y, qv[k].z, qv[k].w};
-                act41_store(act, dyv, myv, ys, b, qs, dv[k], mv_[k]);
-            }
-        }
-    }
-    __syncthreads();            // activation table and ring words ready
-    if (!has) return;
-    auto lds_u32 = [](const unsigned * p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-    auto wait_tag = [&](const unsigned * p, unsigned want) __attribute__((always_inline)) {
-        // every wave of the workgroup is resident: the tag arrives; bounded all the same
-        for (int spins = 0; lds_u32(p) < want && spins < (1 << 22); ++spins) __builtin_amdgcn_s_sleep(1);
-    };
-    const bool even = (j & 1) == 0;
-
-    if (!consumer) {
-        // ---- producer pk of row group gi: chunks pk, pk + NPR, ...
-        if (CPP > 1) issue(1, 1);
-        const uint32_t * ys32 = (const uint32_t *) ys;
-#pragma unroll
-        for (int i = 0; i < CPP; ++i) {
-            const int c = pk + i * NPR;
-            if (c >= NC) break;
-            const int ws = i & 1;
-            const int slot = c % R;
-            uint8_t * sl = gring + (size_t) slot * PC41_SLOT;
-            if (c >= R) wait_tag(freed + gi * R + slot, (unsigned) (c - R + 1));
-            // the four product tables of blocks 32c + 8m + j of row r (ggml.c:2205-2212)
-            {
-                const float4 dy = *(const float4 *) (dyv + c * 32 + j * 4);
-                const float4 my = *(const float4 *) (myv + c * 32 + j * 4);
-                float * tb = (float *) (sl + 64 * PC41_PS) + r * SRS + j;
-                const float dxa[4] = {SD[ws].x, SD[ws].y, SD[ws].z, SD[ws].w};
-                const float mxa[4] = {SM[ws].x, SM[ws].y, SM[ws].z, SM[ws].w};
-                const float dya[4] = {dy.x, dy.y, dy.z, dy.w};
-                const float mya[4] = {my.x, my.y, my.z, my.w};
-#pragma unroll
-                for (int mq = 0; mq < 4; ++mq) {
-                    tb[mq * 8] = dxa[mq] * dya[mq];
-                    tb[SPL + mq * 8] = dxa[mq] * mya[mq];
-                    tb[2 * SPL + mq * 8] = mxa[mq] * dya[mq];
-                    tb[3 * SPL + mq * 8] = mxa[mq] * mya[mq];
-                }
-            }
-            // {p, S} of the chunk's blocks (k_mv_cu41's body): even chains take the weight sums
-            // (blocks 0-15 in their own word, 16-31 in the odd neighbour's), odd chains the
-            // activation sums
-            const uint32_t wown[4] = {WS[ws].x, WS[ws].y, WS[ws].z, WS[ws].w};
-            uint32_t wnb[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) wnb[q] = (uint32_t) __builtin_amdgcn_mov_dpp((int) wown[q], 0xF5, 0xF, 0xF, false);
-            uint32_t ps[32];
-#pragma unroll
-            for (int sb = 0; sb < 4; ++sb) {
-                const uint32_t wd[4] = {W[ws][sb].x, W[ws][sb].y, W[ws][sb].z, W[ws][sb].w};
-#pragma unroll
-                for (int pp = 0; pp < 2; ++pp) {
-                    const int uu = min(c * 8 + sb * 2 + pp, nb / 4 - 1);
-                    const uint4 a = *(const uint4 *) (act + ((size_t) uu * 8 + j) * 4);
-                    const uint32_t ydw = ys32[(size_t) uu * 4 + (j >> 1)];
-                    const uint32_t wdw = sb < 2 ? wown[(sb & 1) * 2 + pp] : wnb[(sb & 1) * 2 + pp];
-                    const uint32_t sdw = even ? wdw : ydw;
-                    const int p[4] = {udot8(wd[2 * pp], a.x), udot8(wd[2 * pp], a.y),
-                                      udot8(wd[2 * pp + 1], a.z), udot8(wd[2 * pp + 1], a.w)};
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const float Sf = (float) ((sdw >> (8 * k)) & 0xFFu);
-                        ps[sb * 8 + pp * 4 + k] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz((float) p[k], Sf));
-                    }
-                }
-            }
-            if (i + 2 < CPP && pk + (i + 2) * NPR < NC) issue(ws, i + 2);
-            uint4 * pd = (uint4 *) (sl + lane * PC41_PS);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) pd[q] = make_uint4(ps[4 * q], ps[4 * q + 1], ps[4 * q + 2], ps[4 * q + 3]);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_store(full + gi * R + slot, (unsigned) (c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        return;
-    }
-
-    // ---- consumer of row group gi: the chains, chunk after chunk, in block order
-    float acc = 0.0f, off = 0.0f;
-#pragma unroll 1
-    for (int c = 0; c < NC; ++c) {
-        const int slot = c % R;
-        const uint8_t * sl = gring + (size_t) slot * PC41_SLOT;
-        wait_tag(full + gi * R + slot, (unsigned) (c + 1));
-        const float * tb = (const float *) (sl + 64 * PC41_PS) + r * SRS;
-        const float * xt = tb + (even ? SPL : 2 * SPL);
-        const float * mt = tb + 3 * SPL;
-        const uint4 * pv = (const uint4 *) (sl + lane * PC41_PS);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {                 // two halves of 16 blocks (register budget)
-            uint32_t ps[16];
-            float s1[16], s2[16], s3[16];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint4 v = pv[h * 4 + q];
-                ps[4 * q] = v.x; ps[4 * q + 1] = v.y; ps[4 * q + 2] = v.z; ps[4 * q + 3] = v.w;
-                const float4 a = *(const float4 *) (tb + h * 16 + q * 4);
-                const float4 x = *(const float4 *) (xt + h * 16 + q * 4);
-                const float4 m = *(const float4 *) (mt + h * 16 + q * 4);
-                s1[4 * q] = a.x; s1[4 * q + 1] = a.y; s1[4 * q + 2] = a.z; s1[4 * q + 3] = a.w;
-                s2[4 * q] = x.x; s2[4 * q + 1] = x.y; s2[4 * q + 2] = x.z; s2[4 * q + 3] = x.w;
-                s3[4 * q] = m.x; s3[4 * q + 1] = m.y; s3[4 * q + 2] = m.z; s3[4 * q + 3] = m.w;
-            }
-            if (h == 1) {
-                // the slot is free once its operands are in registers
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (lane == 0) __hip_atomic_store(freed + gi * R + slot, (unsigned) (c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-#pragma unroll
-            for (int b = 0; b < 16; ++b) {
-                if (c * 4 + (h * 16 + b) / 8 < nsub) {
-                    acc = fma_mix_fh<0>(s1[b], ps[b], acc);        // fmaf(dx*dy, (float) p, acc)
-                    acc = fma_mix_fh<1>(s2[b], ps[b], acc);        // fmaf(cross, (float) S, acc)
-                    off = off + s3[b];                             // acc_offset += mx*my
-                }
-            }
-        }
-    }
-    const float res = octet_reduce(acc) + off * 32.0f;      // acc_offset * QK (ggml.c:2249)
-    const int row = grp * 8 + r;
-    if constexpr (EPI == EPI_STORE) {
-        if (j == 0) P.y[row] = res;
-    } else if constexpr (EPI == EPI_RESID) {
-        if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
-    }
-}
-
-template <int GMAX, int NPR, int R, int PRO, int EPI, int KT>
-hipError_t go_pc41(const Cu41Params & P, hipStream_t s) {
-    static_assert(EPI == EPI_STORE || EPI == EPI_RESID, "k_mv41_pc: store / residual epilogues");
-    constexpr int nb = KT / 32, NC = (nb + 31) / 32, NW = GMAX * (1 + NPR);
-    const int nwg = std::min(cu_count(), P.G);
-    if ((P.G + nwg - 1) / nwg > GMAX) return hipErrorNotSupported;
-    const size_t lds = (size_t) nb * 32 + 2 * NC * 128 + ((nb * 4 + 15) & ~15) + (size_t) GMAX * R * PC41_SLOT +
-                       2 * GMAX * R * 4 + NW * 8;
-    if (lds > 160 * 1024) return hipErrorNotSupported;
-    LVK_LAUNCH((k_mv41_pc<GMAX, NPR, R, PRO, EPI, KT>), dim3(nwg), dim3(NW * 64), lds, s, P);
-    return hipGetLastError();
-}
-
 template <int NW, int D, int PRO, int EPI, int KT, int SPLIT = 0, int HALF = 0>
 hipError_t go(const Cu41Params & P, hipStream_t s) {
     constexpr int nb = KT / 32, NC = (nb + 31) / 32;
@@ -751,16 +443,6 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
     // lm_head would need 14-16 waves = 128 VGPRs, which spills); with 8 waves they prefetch
     // across groups (D = 1: 190 VGPRs, no scratch; measured on 13B: W1|W3 25.2 us vs 27.9
     // at D = 5 and 29.3 for 14 waves, lm_head 27.4 vs 30.1)
-    // producer / consumer form for the 13B Wo and W2 (LVK_MV41_PC=0: one wave per row group)
-    static const int pc_env = [] { const char * e = getenv("LVK_MV41_PC"); return e ? atoi(e) : 1; }();
-    if (pc_env && !half && epi == EPI_RESID) {
-        hipError_t e = hipErrorNotSupported;
-        if (K == 5120 && pro == PRO_ACTQ) e = pc_env == 2 ? go_pc41<3, 2, 3, PRO_ACTQ, EPI_RESID, 5120>(P, s)
-                                                          : go_pc41<3, 3, 3, PRO_ACTQ, EPI_RESID, 5120>(P, s);
-        if (K == 13824 && pro == PRO_ACTF) e = pc_env == 2 ? go_pc41<3, 2, 3, PRO_ACTF, EPI_RESID, 13824>(P, s)
-                                                           : go_pc41<3, 3, 3, PRO_ACTF, EPI_RESID, 13824>(P, s);
-        if (e != hipErrorNotSupported) return e;
-    }
     if (K == 5120) {
         switch (epi) {
             // SPLIT (chunk 1 after the table barrier): 16.9 vs 17.5 us, W2 19.5 vs 19.8

@@ -276,11 +276,17 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
         m.weight_bytes += (size_t) M * (K / 32) * (m.qtype == Q4_0 ? 20 : 24);
         return q;
     };
-    // the prompt matmul's f16 A-fragment images (mm_mfma.hip, 2 B per weight: 13.4 GB for
-    // 7B, 130 GB for 65B): built when they fit next to the Q4 images with 8 GiB to spare
-    // Q4_1: the f16 image plus the per-block side image (mm_mfma41.hip, 3 B per weight in
-    // all) are what the Q4_1 MFMA prompt path runs on; without them its prompts stay on the
-    // VALU kernels
+    // the prompt matmul's f16 A-fragment images (mm_mfma.hip, 2 B per weight: 13.2 GB for
+    // 7B, 130 GB for 65B), decided by capacity (the A-image table):
+    //   * Q4_1: the f16 image plus the per-block side image (mm_mfma41.hip, 3 B per weight in
+    //     all) are what the Q4_1 MFMA prompt path runs on -- 13B 512-token prompt 158 ms with
+    //     them, 1234 ms on the VALU kernels without -- built whenever they fit next to the Q4
+    //     images with 8 GiB to spare;
+    //   * Q4_0: the nibble image runs the same MFMA path only 8-12 % slower (7B 44.3 vs 39.6 ms,
+    //     65B 403 vs 372 ms), so the image (3.2x the Q4 bytes) is built only when it takes at
+    //     most a quarter of the device's memory: 7B / 13B-shaped models and every stage of a
+    //     65B split over 8 GPUs, not the whole 65B on one GPU (130 GB of 288 GB);
+    //     LVK_PROMPT_A16=1 builds it whenever it fits, =0 never
     bool a16 = prompt_a16_env();
     if (a16) {
         const size_t EE = (size_t) E * E, EF = (size_t) E * F;
@@ -290,6 +296,7 @@ void load_model(Model & m, const std::string & path, bool vocab_only, hipStream_
         LVK_HIP(hipMemGetInfo(&free_b, &total_b));
         const size_t q4 = (size_t) ((double) need / per_w * (m.qtype == Q4_0 ? 20.0 : 24.0) / 32.0);
         a16 = free_b > need + q4 + ((size_t) 8 << 30);
+        if (a16 && m.qtype == Q4_0 && !prompt_a16_forced()) a16 = need <= total_b / 4;
     }
     auto repack = [&](QMatrix & q, int interleave4 = 0) {
         LVK_HIP(launch_repack(stage, q.qtype, q.M, q.K, (uint4 *) q.nib, (void *) q.scl, s, interleave4));
