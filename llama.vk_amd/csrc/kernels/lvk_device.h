@@ -140,13 +140,29 @@ __device__ __forceinline__ float rms_mean(double tree, const float * x, int n) {
 // is a multiple of 2^m and the sum is below 2^(m+53), every partial sum in any order is exact,
 // so the tree's sum is the index-order one.  The synthetic models' activations carry few
 // significant bits and often sit exactly on a midpoint, and this certificate covers them.
+#ifdef LVK_PROBE_RMSCOUNT
+// dev probe build only (make rmscount, tools/rms_fallback_count.py): per-translation-unit
+// counters of rms_mean_wave's paths {calls, certificate tried, index-order re-sum}, one count
+// per calling wave
+static __device__ unsigned long long lvk_rms_ctr[3];
+#define LVK_RMS_COUNT(k) do { if ((threadIdx.x & 63) == 0) atomicAdd(&lvk_rms_ctr[k], 1ull); } while (0)
+#define LVK_RMS_ACCESSOR(name)                                                                    \
+    extern "C" __attribute__((visibility("default"))) int name(unsigned long long * out) {        \
+        return (int) hipMemcpyFromSymbol(out, HIP_SYMBOL(::lvk::lvk_rms_ctr), sizeof(::lvk::lvk_rms_ctr));     \
+    }
+#else
+#define LVK_RMS_COUNT(k) do { } while (0)
+#define LVK_RMS_ACCESSOR(name)
+#endif
 __device__ __forceinline__ float rms_mean_wave(double tree, const float * x, int n) {
     const double r = tree / (double) n;
     const uint64_t rb = (uint64_t) __double_as_longlong(r);
     const uint32_t ex = (uint32_t) (rb >> 52);
     const int32_t mid = (int32_t) (uint32_t) (rb & 0x1fffffffu) - (1 << 28);
     const bool safe = rb == 0 || (ex >= 1023 - 126 && ex < 1023 + 128 && (mid > 4 * n || mid < -4 * n));
+    LVK_RMS_COUNT(0);
     if (__builtin_expect(safe, 1)) return (float) r;
+    LVK_RMS_COUNT(1);
     int mlow = 1 << 20;            // lowest set-bit exponent over the nonzero squares
     for (int i = (int) (threadIdx.x & 63); i < n; i += 64) {
         const float v = x[i];
@@ -160,6 +176,7 @@ __device__ __forceinline__ float rms_mean_wave(double tree, const float * x, int
     }
     for (int o = 32; o > 0; o >>= 1) { const int t = __shfl_xor(mlow, o); mlow = t < mlow ? t : mlow; }
     if (mlow == (1 << 20) || tree <= ldexp(1.0, mlow + 52)) return (float) r;
+    LVK_RMS_COUNT(2);
     return rms_mean_in_order(x, n);
 }
 // whole-wave double sum through DPP (quad xor 1, xor 2, half-row and row

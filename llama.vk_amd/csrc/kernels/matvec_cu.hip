@@ -648,3 +648,5 @@ hipError_t launch_matvec_cu(const MvLaunch & L, int pro, int epi, hipStream_t s)
 }
 
 }  // namespace lvk
+
+LVK_RMS_ACCESSOR(lvk_probe_rms_mv)

@@ -491,3 +491,5 @@ hipError_t launch_matvec_cu41(const MvLaunch & L, int pro, int epi, hipStream_t 
 }
 
 }  // namespace lvk
+
+LVK_RMS_ACCESSOR(lvk_probe_rms_mv41)

@@ -473,3 +473,5 @@ hipError_t launch_argmax(const float * x, int n, int * out, hipStream_t s, int *
     return hipGetLastError();
 }
 }  // namespace lvk
+
+LVK_RMS_ACCESSOR(lvk_probe_rms_misc)

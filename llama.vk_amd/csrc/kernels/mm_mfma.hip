@@ -792,3 +792,5 @@ hipError_t launch_rope_kv(const float * qkv, int N, int E, int hd, const float2 
 }
 
 }  // namespace lvk
+
+LVK_RMS_ACCESSOR(lvk_probe_rms_mm)
