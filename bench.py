@@ -607,7 +607,7 @@ def main():
     ap.add_argument("--split-device", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--split-uid", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r06_traffic.json"))
     args = ap.parse_args()
     if args.split_child:
         split_child(args)
