@@ -275,6 +275,11 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     wnb[q] = (uint32_t) __builtin_amdgcn_mov_dpp((int) wown[q], 0xF5, 0xF, 0xF, false);
+#ifdef LVK_PROBE_NOCOMPUTE41   // dev probe build only (make nocomp41): the weights consumed trivially
+                acc += __uint_as_float((W[slot][0].x ^ W[slot][nsub > 1 ? 1 : 0].y ^ WS[slot].z) & 0x3f7fffffu) * SD[slot].x;
+                off += SM[slot].y;
+                if (false)
+#endif
 #pragma unroll
                 for (int sb = 0; sb < 4; ++sb) {
                     if (c * 4 + sb < nsub) {
