@@ -78,3 +78,50 @@ def test_13b_q4_1_full_context_decode_to_511_vs_reference(model13b, ref):
     to the reference's"""
     from test_gpu_7b_full import _full_context
     _full_context(model13b, ref, 511)
+
+
+def test_13b_q4_1_long_context_2048_vs_reference(model13b, ref):
+    """n_ctx 2048 with the second quant format: a 1536-token prompt in 512-token batches (the
+    Q4_1 MFMA prompt path and the prompt attention at n_past 0 / 512 / 1024), then 256
+    teacher-forced decode steps at n_past 1536..1791 (the 40-head decode attention at n_kv up
+    to 1792); every batch's last row and every step's logits bit-identical to the reference"""
+    import lvk
+    from oracle_lib import forced_tokens, prompt_tokens
+    m = lvk.Llama(model13b, n_ctx=2048)
+    rm = ref.model(model13b, 2048)
+    try:
+        toks = prompt_tokens(1536)
+        for c in range(3):
+            part = toks[512 * c:512 * (c + 1)]
+            a = m.eval(part, 512 * c)
+            b = rm.eval(part, 512 * c, n_threads=_threads())
+            assert np.array_equal(bits(a[-1]), bits(b[-1])), "prompt batch %d logits differ" % c
+        seq = forced_tokens(256)
+        bad = []
+        for i, n_past in enumerate(range(1536, 1792)):
+            a = m.eval([int(seq[i])], n_past)
+            b = rm.eval([int(seq[i])], n_past, n_threads=_threads())
+            if not np.array_equal(bits(a[-1]), bits(b[-1])):
+                bad.append(n_past)
+        assert not bad, "decode logits differ at n_past %s" % bad[:20]
+    finally:
+        m.close()
+        rm.close()
+
+
+def test_prompt_image_bytes_follow_the_capacity_rule(model13b):
+    """lvk_prompt_image_bytes: the Q4_1 f16 + side images (3 B per weight of the layer matrices
+    and the lm_head) are built for 13B; LVK_PROMPT_A16=0 builds none"""
+    import lvk
+    E, F, L, V = 5120, 13824, 40, 32000
+    m = lvk.Llama(model13b, n_ctx=64)
+    got = m.prompt_image_bytes()
+    m.close()
+    assert got >= 3 * (L * (4 * E * E + 3 * E * F)), got
+    os.environ["LVK_PROMPT_A16"] = "0"
+    try:
+        m = lvk.Llama(model13b, n_ctx=64)
+        assert m.prompt_image_bytes() == 0
+        m.close()
+    finally:
+        del os.environ["LVK_PROMPT_A16"]
