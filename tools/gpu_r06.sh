@@ -62,6 +62,14 @@ for step in "$@"; do
     env $NOCAP timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
       python3 tools/decode_speed.py 65b 16 > $O/kt65.log 2>&1 || exit 82
     find $O -name '*kernel_stats.csv' ;;
+  split)
+    # the N > 1 bench path rehearsed on one GPU: two ranks (7B replicas + the 65B split leg, one
+    # 40-layer stage per rank over the shm stage link; RCCL needs two devices)
+    timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 5 --split-transport shm --no-13b --no-cpu-baseline \
+      > gpurun_out/r06_bench_split_shm_s2.json 2> gpurun_out/r06_split.err \
+      || { tail -30 gpurun_out/r06_split.err; exit 62; }
+    tail -c 800 gpurun_out/r06_bench_split_shm_s2.json ;;
   *)
     echo "unknown step $step"; exit 2 ;;
   esac
