@@ -138,22 +138,28 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
     LVK_DT(0);
     // the step block through the scalar cache (constant address space: s_load, counted by
     // lgkmcnt): a vector load here would retire behind every Q / K / V load issued below
-    // (vmcnt is in order) and hold the n_kv-dependent loads back by a full HBM latency
+    // (vmcnt is in order) and hold the n_kv-dependent loads back by a full HBM latency.  Both
+    // words are read here, ahead of the Q loads (the sched barriers keep the scalar loads in
+    // front and their first use -- and wait -- behind the Q issue): with the granule tag
+    // computed up front, hipcc waited for the step block before issuing anything
     const __attribute__((address_space(4))) StepParams * spc = (const __attribute__((address_space(4))) StepParams *) A.sp;
     const int n_past = spc->n_past;
-    // this layer's granule tag: unique per (step, layer) when the step counter is used
-    const unsigned ep = A.seq_epochs ? A.epoch + (spc->seq << 7) : A.epoch;
+    const unsigned seqv = spc->seq;
+    __builtin_amdgcn_sched_barrier(0);
 
-    // 1a. Loads that do not depend on n_past go out before the step block is read: Q and
-    // the K rows of positions 0..63 (chunk 0; rows past n_kv are read, never used).  A short
-    // context (n_kv <= 64, no exchange) then has its score operands in flight from the
-    // first cycle; V follows behind the first scores (1b).
+    // 1a. Q goes out before the step block is known; V follows behind the first scores (1b)
     uint4 qv[4];
     {
         const uint4 * qp = (const uint4 *) (A.q16 + h * HD) + r;
 #pragma unroll
         for (int st = 0; st < 4; ++st) qv[st] = qp[st * 4];
     }
+    LVK_DT(13);
+    __builtin_amdgcn_sched_barrier(0);
+#ifdef LVK_PROBE_TIMING
+    asm volatile("" ::"s"(n_past));
+    LVK_DT(12);
+#endif
     auto v_dma = [&](int p0, int lo, int lim) {     // positions [max(p0, lo), min(p0 + 512, lim)) of rows 8 wave ..
 #pragma unroll
         for (int i = 0; i < 8; ++i) {               // a static count: the score waits can count past it
@@ -164,33 +170,25 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
                                                  16, 0, 0);
         }
     };
-    uint4 kv[2][4];
-    {
-        const int p = min(tid >> 2, n_ctx - 1);
-        const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
-#pragma unroll
-        for (int st = 0; st < 4; ++st) kv[0][st] = kp[st * 4];
-    }
+    // this layer's granule tag: unique per (step, layer) when the step counter is used
+    const unsigned ep = A.epoch + (A.seq_epochs ? seqv << 7 : 0u);
     const int n_kv = n_past + 1;
     const int n_pad = (n_kv + 31) & ~31;
     const int np = n_kv & ~31;
     const bool exch = DYN ? n_kv > A.short_max : true;
-    // the rest of this workgroup's first two K chunks; chunk 0 of an exchange is positions
-    // sl*64.. and lands in registers of its own (a reload into kv[0] would have to wait for
-    // the speculative load first)
-    const bool c0_other = exch && sl > 0;
-    uint4 kx[4];
-    if (c0_other) {
-        const int p = min(sl * 64 + (tid >> 2), n_kv - 1);
+    const int cs = exch ? 256 : 64;                     // position stride of this workgroup's chunks
+    const int cb = exch ? sl * 64 : 0;                  // its first chunk
+    // this workgroup's first two K chunks, issued once n_past is known.  (A speculative load
+    // of positions 0..63 before the step block, which only the short schedule and workgroup 0
+    // use, measured 0.1-0.25 us slower per launch: it queued ahead of the chunks an exchange
+    // workgroup needs; profiles/r06/decode_ab/)
+    uint4 kv[2][4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int p = min(cb + k * cs + (tid >> 2), n_kv - 1);
         const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
 #pragma unroll
-        for (int st = 0; st < 4; ++st) kx[st] = kp[st * 4];
-    }
-    {
-        const int p = min((exch ? sl * 64 + 256 : 64) + (tid >> 2), n_kv - 1);
-        const uint4 * kp = (const uint4 *) (A.kc + (size_t) p * E + h * HD) + r;
-#pragma unroll
-        for (int st = 0; st < 4; ++st) kv[1][st] = kp[st * 4];
+        for (int st = 0; st < 4; ++st) kv[k][st] = kp[st * 4];
     }
     LVK_DT(6);
 
@@ -219,10 +217,7 @@ __device__ __forceinline__ void attn_d_run(const AttnDArgs & A, const int h, con
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
         };
-        const int cs = exch ? 256 : 64;                     // position stride of this workgroup's chunks
-        const int cb = exch ? sl * 64 : 0;
-        if (c0_other) score(kx, cb + (tid >> 2));
-        else score(kv[0], cb + (tid >> 2));          // cb < n_kv: sl * 64 < n_kv when c0_other
+        score(kv[0], cb + (tid >> 2));               // positions past n_kv publish nothing
         if (cb + cs < n_kv) score(kv[1], cb + cs + (tid >> 2));
         // the V slice goes out behind the first two chunks' scores: those wait only for their
         // own K rows, the V rows are needed after the softmax.  (Chunk 0 of V issued with Q

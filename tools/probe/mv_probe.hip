@@ -231,7 +231,7 @@ int main(int argc, char ** argv) {
                 t0min = std::min(t0min, e[0]); t0max = std::max(t0max, e[0]); tend = std::max(tend, e[11]);
                 for (int k = 1; k < 14; k++) { acc[k] += (double) (e[k] - e[0]); mxv[k] = std::max(mxv[k], (double) (e[k] - e[0])); }
             }
-            const char * nm[14] = {"", "dma-issued", "scores", "exchange", "softmax", "dma-wait", "qk-issued", "v-dma", "max-sync", "sum-sync", "pv", "end", "npast-known", "k0-issued"};
+            const char * nm[14] = {"", "dma-issued", "scores", "exchange", "softmax", "dma-wait", "qk-issued", "v-dma", "max-sync", "sum-sync", "pv", "end", "npast-known", "q-issued"};
             const int ord[13] = {12, 13, 6, 7, 1, 2, 3, 8, 9, 4, 5, 10, 11};
             printf("decode attention trace (%d waves, entry spread %llu, first entry -> last end %llu cycles), avg (max) from wave entry:\n ",
                    n, t0max - t0min, tend - t0min);
