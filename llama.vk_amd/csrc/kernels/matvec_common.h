@@ -237,6 +237,25 @@ __device__ __forceinline__ void qkv_epilogue(float res, int row, int j, int E, i
     }
 }
 
+// qkv_epilogue with the lane's RoPE pair already loaded (cs: rope[pos * hd / 2 + (e % hd) / 2])
+__device__ __forceinline__ void qkv_epilogue_cs(float res, int row, int j, int E, int hd, int pos, float2 cs,
+                                                uint16_t * q16, uint16_t * kc, uint16_t * vc, int n_ctx, int kv32) {
+    const int which = row / E;
+    const int e = row - which * E;
+    const float other = __shfl_xor(res, 8);
+    float out = res;
+    if (which < 2) {
+        const int i0 = e % hd;
+        if ((i0 & 1) == 0) { const float a = res * cs.x, b = other * cs.y; out = a - b; }
+        else               { const float a = other * cs.y, b = res * cs.x; out = a + b; }
+    }
+    if (j == 0) {
+        if (which == 0)      kv_store(q16, e, out, kv32);
+        else if (which == 1) kv_store(kc, (size_t) pos * E + e, out, kv32);
+        else                 kv_store(vc, (size_t) e * n_ctx + pos, out, kv32);
+    }
+}
+
 }  // namespace mv
 // the RoPE + KV epilogue of a prompt-matmul lane (mm_mfma.hip, mm_mfma41.hip): the lane holds
 // rows m0 + 32w + 8q + 4h + p (p = 0..3) of token n; rows [0, E) Q, [E, 2E) K, [2E, 3E) V.

@@ -187,6 +187,14 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
     const int ng = max(0, (g1 - g0 - wave + NW - 1) / NW);      // row groups of this wave
     if (NP > 0 && ng == 0) { __builtin_amdgcn_s_barrier(); __syncthreads(); return; }
     int gc = min(g0 + wave, P.G - 1);
+    // the QKV epilogue's position, loaded here ahead of the prologue inputs (vmcnt retires in
+    // order: the inputs' wait covers it), so that the RoPE pair can be loaded at a row group's
+    // start (pre_epi below).  An atomic load: a plain one is sunk to its use; a scalar one sinks
+    // too and then holds up the prologue's first barrier, whose lgkmcnt wait covers it.
+    [[maybe_unused]] int pos0 = 0;
+    if constexpr (EPI == EPI_QKV)
+        pos0 = __hip_atomic_load((const __attribute__((address_space(1))) int *) &P.sp->n_past, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
 
     // NP == 0: the compute waves build the activation table themselves; its
     // inputs are issued first (vmcnt retires in order)
@@ -454,15 +462,31 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
         return octet_reduce(acc);
     };
 
-    auto epilogue = [&](int grp, float res) __attribute__((always_inline)) {
+    // the epilogue's memory operand of a row group -- the lane's RoPE pair, or the residual term --
+    // issued before the group's chunk loop: loaded in the epilogue it was a full memory round
+    // trip in every wave's tail (QKV 7.60 -> 7.45, Wo 4.41 -> 4.25, W2 7.33 -> 7.26 us;
+    // profiles/r06/decode_ab/epilogue_summary.txt)
+    struct EpiPre { float2 cs; float rv; };
+    auto pre_epi = [&](int grp) __attribute__((always_inline)) {
+        EpiPre e{make_float2(0.0f, 0.0f), 0.0f};
+        if constexpr (EPI == EPI_QKV) {
+            const int row = grp * 8 + r;
+            const int i0 = (row - (row / P.n_embd) * P.n_embd) % P.head_dim;   // V rows: an unused pair
+            e.cs = P.rope[(size_t) pos0 * (P.head_dim / 2) + (i0 >> 1)];
+        } else if constexpr (EPI == EPI_RESID) {
+            e.rv = P.y[grp * 8 + r];
+        }
+        return e;
+    };
+    auto epilogue = [&](int grp, float res, const EpiPre & pe) __attribute__((always_inline)) {
         const int row = grp * 8 + r;
         if constexpr (EPI == EPI_STORE) {
             if (j == 0) P.y[row] = res;
         } else if constexpr (EPI == EPI_RESID) {
-            if (j == 0) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+            // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+            if (j == 0) P.y[row] = res + pe.rv;
         } else if constexpr (EPI == EPI_QKV) {
-            const StepParams * sp = P.sp;
-            qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32);
+            qkv_epilogue_cs(res, row, j, P.n_embd, P.head_dim, pos0, pe.cs, P.q16, P.kc, P.vc, P.n_ctx, P.kv32);
         } else if constexpr (EPI == EPI_SWIGLU_F32) {
             // fused W1|W3 image interleaved per 4 rows: rows 0-3 of the group are
             // w1 rows 4grp..4grp+3, rows 4-7 the w3 rows (llama.cpp:1085-1096)
@@ -478,13 +502,15 @@ __device__ __forceinline__ void mv_cu_run(const CuParams & P, const int bid, con
     __builtin_amdgcn_wave_barrier();
     if constexpr (XG) {
         for (int k = 0; k + 1 < ng; ++k) {
+            const EpiPre pe = pre_epi(gc);
             const float res = body(std::true_type{}, gc, gc + NW);
-            epilogue(gc, res);
+            epilogue(gc, res, pe);
             gc += NW;
         }
     }
+    const EpiPre pe = pre_epi(gc);
     const float res = body(std::false_type{}, gc, gc);
-    epilogue(gc, res);
+    epilogue(gc, res, pe);
     LVK_T(3);
 #undef LVK_ISSUE
 }

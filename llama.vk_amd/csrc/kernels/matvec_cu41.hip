@@ -107,6 +107,12 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     };
     const uint32_t lp = (uint32_t) (lane & 31) * 16u;
     int gc = wave;           // item index of the wave's current row group / half-group pair
+    // the QKV epilogue's position, loaded ahead of the inputs so that the RoPE pair can be loaded at
+    // an item's start (pre_epi; matvec_cu.hip has the measurements)
+    [[maybe_unused]] int pos0 = 0;
+    if constexpr (EPI == EPI_QKV)
+        pos0 = __hip_atomic_load((const __attribute__((address_space(1))) int *) &P.sp->n_past, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
 
     // activation inputs first (vmcnt retires in order)
     constexpr bool FPRO = (PRO == PRO_NORM || PRO == PRO_ACTF);
@@ -322,7 +328,25 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
         return octet_reduce(acc);
     };
 
-    auto epilogue = [&](int item, float h, float off) __attribute__((always_inline)) {
+    // the epilogue's memory operand of an item (the lane's RoPE pair, or the residual term), loaded
+    // before the item's chunk loop instead of in the wave's tail (as matvec_cu.hip)
+    struct EpiPre { float2 cs; float rv; };
+    auto pre_epi = [&](int item) __attribute__((always_inline)) {
+        EpiPre e{make_float2(0.0f, 0.0f), 0.0f};
+        if constexpr (EPI == EPI_QKV || EPI == EPI_RESID) {
+            bool valid;
+            const int u = unit_of(item, valid);
+            const int row = (u >> 1) * 8 + (u & 1) * 4 + (r & 3);
+            if constexpr (EPI == EPI_QKV) {
+                const int i0 = (row - (row / P.n_embd) * P.n_embd) % P.head_dim;   // V rows: an unused pair
+                e.cs = P.rope[(size_t) pos0 * (P.head_dim / 2) + (i0 >> 1)];
+            } else {
+                e.rv = P.y[row];
+            }
+        }
+        return e;
+    };
+    auto epilogue = [&](int item, float h, float off, const EpiPre & pe) __attribute__((always_inline)) {
         const float res = h + off * 32.0f;        // acc_offset * QK (ggml.c:2249)
         bool valid;
         const int u = unit_of(item, valid);
@@ -331,12 +355,11 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
         if constexpr (EPI == EPI_STORE) {
             if (j == 0 && valid) P.y[row] = res;
         } else if constexpr (EPI == EPI_RESID) {
-            if (j == 0 && valid) P.y[row] = res + P.y[row];      // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
+            if (j == 0 && valid) P.y[row] = res + pe.rv;         // ggml_add(cur, inpSA) (llama.cpp:1071,1103)
         } else if constexpr (EPI == EPI_QKV) {
             // (a duplicated half, !valid, recomputed its original's rows bit for bit: its stores
             // write the same values, and the RoPE partner exchange stays convergent)
-            const StepParams * sp = P.sp;
-            qkv_epilogue(res, row, j, P.n_embd, P.head_dim, sp->n_past, P.rope, P.q16, P.kc, P.vc, P.n_ctx, P.kv32);
+            qkv_epilogue_cs(res, row, j, P.n_embd, P.head_dim, pos0, pe.cs, P.q16, P.kc, P.vc, P.n_ctx, P.kv32);
         } else if constexpr (EPI == EPI_SWIGLU_F32) {
             // fused W1|W3 image interleaved per 4 rows: rows 0-3 of the group are
             // w1 rows 4grp..4grp+3, rows 4-7 the w3 rows (llama.cpp:1085-1096)
@@ -351,15 +374,17 @@ __global__ __launch_bounds__(NW * 64) void k_mv_cu41(Cu41Params P) {
     if constexpr (XG) {
         for (int k = 0; k + 1 < ng; ++k) {
             float off;
+            const EpiPre pe = pre_epi(gc);
             const float h = body(std::true_type{}, off);
-            epilogue(gc, h, off);
+            epilogue(gc, h, off, pe);
             gc += NW;
             lane_bases(gc, lb_n, lb_s, lb_w);
         }
     }
     float off;
+    const EpiPre pe = pre_epi(gc);
     const float h = body(std::false_type{}, off);
-    epilogue(gc, h, off);
+    epilogue(gc, h, off, pe);
 #undef LVK_ISSUE41
 }
 

@@ -14,6 +14,40 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+@pytest.fixture(autouse=True)
+def _gpu_heartbeat(request):
+    """While a GPU test runs, append a line to gpurun_out/pytest_heartbeat.log every 20 s. The
+    full-size parity tests run the reference CPU build for minutes (the 65B 512-token prompt
+    at -t 16 takes ~3 min on a slow host) and print nothing meanwhile; the GPU-box runner
+    takes a command that writes nothing to stdout, stderr or gpurun_out/ for 3 minutes to be
+    hung and kills it."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import threading
+    import time
+    d = os.path.join(ROOT, "gpurun_out")
+    stop = threading.Event()
+
+    def beat():
+        t0 = time.time()
+        while not stop.wait(20.0):
+            try:
+                os.makedirs(d, exist_ok=True)
+                with open(os.path.join(d, "pytest_heartbeat.log"), "a") as f:
+                    f.write("%s %.0f s\n" % (request.node.nodeid, time.time() - t0))
+            except OSError:
+                pass
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        yield
+    finally:
+        stop.set()
+        th.join(timeout=5)
+
+
 def _ensure_built():
     if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "oracle"], stdout=subprocess.DEVNULL)
